@@ -1,0 +1,394 @@
+// C-ABI of libdiloco_hip.so (include/diloco_hip.h): argument checking, the layout planner,
+// tree handles (chunk table + device pointer tables) and kernel dispatch.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "dl_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  return fail(int(e), "%s: %s (%s)", where, hipGetErrorName(e), hipGetErrorString(e));
+}
+
+#define DL_HIP(call, where)                          \
+  do {                                               \
+    hipError_t e_ = (call);                          \
+    if (e_ != hipSuccess) return hip_fail(e_, where); \
+  } while (0)
+
+int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+// The planner rule (frozen; bit-exact contract with oracle/diloco_oracle.c:or_plan_tables and
+// diloco_amd/plan.py). Returns number of buckets.
+int plan(const int64_t* numel, int32_t n, int64_t cap, int32_t align, int64_t* seg_off,
+         int64_t* bounds) {
+  seg_off[0] = 0;
+  for (int32_t i = 0; i < n; ++i) seg_off[i + 1] = align_up(seg_off[i] + numel[i], align);
+  if (n == 0) {
+    bounds[0] = 0;
+    return 0;
+  }
+  int nb = 0;
+  bounds[0] = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const int64_t start = bounds[nb];
+    if (cap > 0 && i > start && seg_off[i + 1] - seg_off[start] > cap) bounds[++nb] = i;
+  }
+  bounds[++nb] = n;
+  return nb;
+}
+
+}  // namespace
+
+struct dl_tree_s {
+  int device = 0;
+  int32_t nseg = 0;
+  int64_t total = 0;
+  std::vector<int64_t> numel, seg_off, bounds;
+  std::vector<int32_t> bkt_chunk;  // first chunk of each bucket, + sentinel
+  std::vector<dl::Chunk> chunks;
+  dl::Chunk* d_chunks = nullptr;
+  void** d_ptab = nullptr;
+  uint64_t* h_stage = nullptr;  // pinned staging for pointer-table uploads
+  std::vector<uint8_t> bound;   // slot bound?
+  std::vector<uint8_t> slot_aligned;
+  int32_t grid = 0;
+};
+
+extern "C" {
+
+DL_API const char* dl_last_error(void) { return g_err.c_str(); }
+DL_API int dl_abi_version(void) { return DL_ABI_VERSION; }
+
+DL_API int dl_plan_tables(const int64_t* numel, int32_t n, int64_t cap_elems, int32_t align_elems,
+                          int64_t* seg_off, int64_t* bkt_bounds, int32_t* n_bkt) {
+  if (n < 0 || (n > 0 && !numel) || !seg_off || !bkt_bounds || !n_bkt)
+    return fail(DL_E_ARG, "dl_plan_tables: null pointer or n < 0");
+  if (align_elems <= 0) return fail(DL_E_ARG, "dl_plan_tables: align_elems must be > 0");
+  for (int32_t i = 0; i < n; ++i)
+    if (numel[i] < 0) return fail(DL_E_ARG, "dl_plan_tables: numel[%d] < 0", i);
+  *n_bkt = plan(numel, n, cap_elems, align_elems, seg_off, bkt_bounds);
+  return DL_OK;
+}
+
+DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl_tree_t* out) {
+  if (!out) return fail(DL_E_ARG, "dl_tree_create: out is null");
+  *out = nullptr;
+  if (n < 0 || (n > 0 && !numel)) return fail(DL_E_ARG, "dl_tree_create: bad numel/n");
+  dl_tree_s* t = new (std::nothrow) dl_tree_s;
+  if (!t) return fail(DL_E_STATE, "dl_tree_create: out of host memory");
+  t->nseg = n;
+  t->numel.assign(numel, numel + n);
+  t->seg_off.resize(size_t(n) + 1);
+  t->bounds.resize(size_t(n) + 1);
+  int32_t nb = 0;
+  int rc = dl_plan_tables(numel, n, cap_elems, DL_ALIGN_ELEMS, t->seg_off.data(), t->bounds.data(),
+                          &nb);
+  if (rc) {
+    delete t;
+    return rc;
+  }
+  t->bounds.resize(size_t(nb) + 1);
+  t->total = t->seg_off[t->nseg];
+  // chunk table, bucket-major (buckets are contiguous runs of segments)
+  t->bkt_chunk.resize(size_t(nb) + 1);
+  for (int32_t b = 0; b < nb; ++b) {
+    t->bkt_chunk[b] = int32_t(t->chunks.size());
+    for (int64_t s = t->bounds[b]; s < t->bounds[b + 1]; ++s) {
+      for (int64_t off = 0; off < t->numel[s]; off += DL_CHUNK_ELEMS) {
+        dl::Chunk c{};
+        c.poff = t->seg_off[s] + off;
+        c.loff = off;
+        c.seg = int32_t(s);
+        const int64_t rem = t->numel[s] - off;
+        c.len = int32_t(rem < DL_CHUNK_ELEMS ? rem : DL_CHUNK_ELEMS);
+        t->chunks.push_back(c);
+      }
+    }
+    if (t->chunks.size() > size_t(INT32_MAX)) {
+      delete t;
+      return fail(DL_E_ARG, "dl_tree_create: tree too large for int32 chunk indices");
+    }
+  }
+  t->bkt_chunk[nb] = int32_t(t->chunks.size());
+  t->bound.assign(DL_MAX_SLOTS, 0);
+  t->slot_aligned.assign(DL_MAX_SLOTS, 1);
+
+  hipError_t e = hipGetDevice(&t->device);
+  if (e == hipSuccess) {
+    int cus = 0;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device);
+    t->grid = (cus > 0 ? cus : 256) * 8;
+  }
+  const size_t cbytes = (t->chunks.empty() ? 1 : t->chunks.size()) * sizeof(dl::Chunk);
+  const size_t pbytes = size_t(DL_MAX_SLOTS) * (t->nseg > 0 ? t->nseg : 1) * sizeof(void*);
+  if (e == hipSuccess) e = hipMalloc(&t->d_chunks, cbytes);
+  if (e == hipSuccess) e = hipMalloc(&t->d_ptab, pbytes);
+  if (e == hipSuccess) e = hipMemset(t->d_ptab, 0, pbytes);
+  if (e == hipSuccess && !t->chunks.empty())
+    e = hipMemcpy(t->d_chunks, t->chunks.data(), t->chunks.size() * sizeof(dl::Chunk),
+                  hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&t->h_stage),
+                      (t->nseg > 0 ? t->nseg : 1) * sizeof(uint64_t), hipHostMallocDefault);
+  if (e != hipSuccess) {
+    int rc2 = hip_fail(e, "dl_tree_create");
+    dl_tree_destroy(t);
+    return rc2;
+  }
+  *out = t;
+  return DL_OK;
+}
+
+DL_API int dl_tree_destroy(dl_tree_t t) {
+  if (!t) return DL_OK;
+  if (t->d_chunks) (void)hipFree(t->d_chunks);
+  if (t->d_ptab) (void)hipFree(t->d_ptab);
+  if (t->h_stage) (void)hipHostFree(t->h_stage);
+  delete t;
+  return DL_OK;
+}
+
+DL_API int dl_tree_query(dl_tree_t t, int64_t* total, int32_t* nseg, int32_t* nbkt,
+                         int32_t* nchunk) {
+  if (!t) return fail(DL_E_ARG, "dl_tree_query: null tree");
+  if (total) *total = t->total;
+  if (nseg) *nseg = t->nseg;
+  if (nbkt) *nbkt = int32_t(t->bounds.size()) - 1;
+  if (nchunk) *nchunk = int32_t(t->chunks.size());
+  return DL_OK;
+}
+
+DL_API int dl_tree_seg_off(dl_tree_t t, int64_t* seg_off) {
+  if (!t || !seg_off) return fail(DL_E_ARG, "dl_tree_seg_off: null argument");
+  std::memcpy(seg_off, t->seg_off.data(), t->seg_off.size() * sizeof(int64_t));
+  return DL_OK;
+}
+
+DL_API int dl_tree_bucket_range(dl_tree_t t, int32_t b, int64_t* begin, int64_t* end) {
+  if (!t || !begin || !end) return fail(DL_E_ARG, "dl_tree_bucket_range: null argument");
+  const int32_t nb = int32_t(t->bounds.size()) - 1;
+  if (b == DL_ALL_BUCKETS) {
+    *begin = 0;
+    *end = t->total;
+    return DL_OK;
+  }
+  if (b < 0 || b >= nb) return fail(DL_E_ARG, "dl_tree_bucket_range: bucket %d of %d", b, nb);
+  *begin = t->seg_off[t->bounds[b]];
+  *end = t->seg_off[t->bounds[b + 1]];
+  return DL_OK;
+}
+
+DL_API int dl_tree_set_grid(dl_tree_t t, int32_t max_blocks) {
+  if (!t || max_blocks < 0) return fail(DL_E_ARG, "dl_tree_set_grid: bad argument");
+  if (max_blocks == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device) !=
+        hipSuccess)
+      cus = 256;
+    t->grid = cus * 8;
+  } else {
+    t->grid = max_blocks;
+  }
+  return DL_OK;
+}
+
+DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t n,
+                        dl_stream_t stream) {
+  if (!t) return fail(DL_E_ARG, "dl_tree_bind: null tree");
+  if (slot < 0 || slot >= DL_MAX_SLOTS) return fail(DL_E_ARG, "dl_tree_bind: slot %d", slot);
+  if (n != t->nseg) return fail(DL_E_ARG, "dl_tree_bind: %d pointers for %d tensors", n, t->nseg);
+  if (n > 0 && !ptrs) return fail(DL_E_ARG, "dl_tree_bind: null pointer array");
+  for (int32_t i = 0; i < n; ++i) {
+    if (ptrs[i] == 0 && t->numel[i] > 0)
+      return fail(DL_E_ARG, "dl_tree_bind: null address for tensor %d", i);
+    if (ptrs[i] & 3u) return fail(DL_E_ALIGN, "dl_tree_bind: tensor %d not 4-B aligned", i);
+  }
+  if (n == 0) {
+    t->bound[slot] = 1;
+    return DL_OK;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // The previous table of this slot may still be read by queued kernels on `s`: the copy is
+  // stream-ordered behind them; the staging buffer is reused only after it has landed.
+  DL_HIP(hipStreamSynchronize(s), "dl_tree_bind(sync before stage)");
+  std::memcpy(t->h_stage, ptrs, size_t(n) * sizeof(uint64_t));
+  DL_HIP(hipMemcpyAsync(t->d_ptab + size_t(slot) * t->nseg, t->h_stage, size_t(n) * sizeof(void*),
+                        hipMemcpyHostToDevice, s),
+         "dl_tree_bind(upload)");
+  DL_HIP(hipStreamSynchronize(s), "dl_tree_bind(sync after upload)");
+  t->bound[slot] = 1;
+  return DL_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who) {
+  if (!t) return fail(DL_E_ARG, "%s: null tree", who);
+  const int32_t nb = int32_t(t->bounds.size()) - 1;
+  if (b == DL_ALL_BUCKETS) {
+    L->c0 = 0;
+    L->c1 = int32_t(t->chunks.size());
+  } else if (b >= 0 && b < nb) {
+    L->c0 = t->bkt_chunk[b];
+    L->c1 = t->bkt_chunk[b + 1];
+  } else {
+    return fail(DL_E_ARG, "%s: bucket %d of %d", who, b, nb);
+  }
+  L->chunks = t->d_chunks;
+  L->ptab = t->d_ptab;
+  L->nseg = t->nseg;
+  L->grid = t->grid > 0 ? t->grid : 2048;
+  L->stream = static_cast<hipStream_t>(s);
+  return DL_OK;
+}
+
+int check_slot(dl_tree_t t, int32_t slot, const char* who, bool optional = false) {
+  if (optional && slot < 0) return DL_OK;
+  if (slot < 0 || slot >= DL_MAX_SLOTS) return fail(DL_E_ARG, "%s: slot %d", who, slot);
+  if (!t->bound[slot]) return fail(DL_E_STATE, "%s: slot %d not bound", who, slot);
+  return DL_OK;
+}
+
+int check_packed(const void* p, const char* who, const char* what) {
+  if (!p) return fail(DL_E_ARG, "%s: %s is null", who, what);
+  if (!dl::aligned16_host(p)) return fail(DL_E_ALIGN, "%s: %s not 16-B aligned", who, what);
+  return DL_OK;
+}
+
+int check_dtype(int32_t d, const char* who) {
+  if (d != DL_F32 && d != DL_BF16) return fail(DL_E_ARG, "%s: wire dtype %d", who, d);
+  return DL_OK;
+}
+
+#define DL_TRY(x)         \
+  do {                    \
+    int rc_ = (x);        \
+    if (rc_) return rc_;  \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+DL_API int dl_delta_pack(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,
+                         void* wire, int32_t wire_dtype, dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack"));
+  DL_TRY(check_slot(t, inner_slot, "dl_delta_pack"));
+  DL_TRY(check_packed(outer, "dl_delta_pack", "outer"));
+  DL_TRY(check_packed(wire, "dl_delta_pack", "wire"));
+  DL_TRY(check_dtype(wire_dtype, "dl_delta_pack"));
+  hipError_t e = dl::launch_delta_pack(L, inner_slot, outer, wire, wire_dtype);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_pack");
+}
+
+DL_API int dl_unpack_avg(dl_tree_t t, int32_t b, const void* wire, int32_t wire_dtype,
+                         int32_t divisor, int32_t dst_slot, float* dst_packed, dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_avg"));
+  DL_TRY(check_packed(wire, "dl_unpack_avg", "wire"));
+  DL_TRY(check_dtype(wire_dtype, "dl_unpack_avg"));
+  if (divisor < 1) return fail(DL_E_ARG, "dl_unpack_avg: divisor %d", divisor);
+  if (dst_slot >= 0)
+    DL_TRY(check_slot(t, dst_slot, "dl_unpack_avg"));
+  else
+    DL_TRY(check_packed(dst_packed, "dl_unpack_avg", "dst_packed"));
+  hipError_t e = dl::launch_unpack_avg(L, wire, wire_dtype, divisor, dst_slot, dst_packed);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_unpack_avg");
+}
+
+DL_API int dl_unpack_sgd(dl_tree_t t, int32_t b, const void* wire, int32_t wire_dtype,
+                         int32_t divisor, float* outer, float* mom, float lr, float momentum,
+                         int32_t nesterov, int32_t first_step, int32_t inner_slot,
+                         dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd"));
+  DL_TRY(check_packed(wire, "dl_unpack_sgd", "wire"));
+  DL_TRY(check_dtype(wire_dtype, "dl_unpack_sgd"));
+  DL_TRY(check_packed(outer, "dl_unpack_sgd", "outer"));
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_unpack_sgd", "momentum"));
+  DL_TRY(check_slot(t, inner_slot, "dl_unpack_sgd", true));
+  if (divisor < 1) return fail(DL_E_ARG, "dl_unpack_sgd: divisor %d", divisor);
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_unpack_sgd: Nesterov momentum requires a momentum");
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_unpack_sgd(L, wire, wire_dtype, divisor, outer, mom, a, inner_slot);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_unpack_sgd");
+}
+
+DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int32_t dtype,
+                     dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_gather"));
+  DL_TRY(check_slot(t, src_slot, "dl_gather"));
+  DL_TRY(check_packed(packed, "dl_gather", "packed"));
+  DL_TRY(check_dtype(dtype, "dl_gather"));
+  hipError_t e = dl::launch_gather(L, src_slot, packed, dtype);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_gather");
+}
+
+DL_API int dl_scatter(dl_tree_t t, int32_t b, const float* packed, int32_t dst_slot,
+                      dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_scatter"));
+  DL_TRY(check_slot(t, dst_slot, "dl_scatter"));
+  DL_TRY(check_packed(packed, "dl_scatter", "packed"));
+  hipError_t e = dl::launch_scatter(L, packed, dst_slot);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_scatter");
+}
+
+DL_API int dl_serialize(const void* src, int32_t src_dtype, int64_t numel, float meta0,
+                        float meta1, float* out, dl_stream_t s) {
+  if (!src || !out) return fail(DL_E_ARG, "dl_serialize: null pointer");
+  if (numel < 2) return fail(DL_E_ARG, "dl_serialize: numel %lld < 2", (long long)numel);
+  if (src_dtype != DL_F32 && src_dtype != DL_BF16 && src_dtype != DL_F16)
+    return fail(DL_E_ARG, "dl_serialize: dtype %d", src_dtype);
+  hipError_t e = dl::launch_serialize(src, src_dtype, numel, meta0, meta1, out,
+                                      static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_serialize");
+}
+
+DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id, float base,
+                         float scale, const float* add, dl_stream_t s) {
+  if (n < 0 || (n > 0 && !dst)) return fail(DL_E_ARG, "dl_fill_synth: bad dst/n");
+  if (stream_id >= (1ull << 24)) return fail(DL_E_ARG, "dl_fill_synth: stream_id >= 2^24");
+  if (n >= (1ll << 40)) return fail(DL_E_ARG, "dl_fill_synth: n >= 2^40");
+  hipError_t e = dl::launch_fill_synth(dst, n, seed, stream_id, base, scale, add,
+                                       static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_fill_synth");
+}
+
+DL_API int dl_host_register(void* ptr, int64_t bytes) {
+  if (!ptr || bytes <= 0) return fail(DL_E_ARG, "dl_host_register: bad range");
+  DL_HIP(hipHostRegister(ptr, size_t(bytes), hipHostRegisterDefault), "dl_host_register");
+  return DL_OK;
+}
+
+DL_API int dl_host_unregister(void* ptr) {
+  if (!ptr) return fail(DL_E_ARG, "dl_host_unregister: null");
+  DL_HIP(hipHostUnregister(ptr), "dl_host_unregister");
+  return DL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// Internal declarations shared by the kernel TU (dl_kernels.hip) and the C-ABI TU (dl_abi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/diloco_hip.h"
+
+namespace dl {
+
+constexpr int kThreads = 256;                          // 4 waves of 64 lanes
+constexpr int kUnroll = DL_CHUNK_ELEMS / (kThreads * 4);  // float4 per lane per chunk (=4)
+static_assert(kUnroll * kThreads * 4 == DL_CHUNK_ELEMS, "chunk must be a whole number of sweeps");
+
+// One work unit: up to DL_CHUNK_ELEMS consecutive elements of one segment. 32 B so a
+// workgroup fetches it with one scalar load.
+struct Chunk {
+  int64_t poff;  // offset in the packed space
+  int64_t loff;  // offset inside the segment's own tensor
+  int32_t seg;   // segment (tensor) index in parameters() order
+  int32_t len;   // elements, 1..DL_CHUNK_ELEMS
+  int64_t pad_;
+};
+static_assert(sizeof(Chunk) == 32, "Chunk layout");
+
+inline bool aligned16_host(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+struct SgdArgs {
+  float neg_lr;    // fp32(-lr): torch passes alpha=-lr, rounded to the tensor dtype
+  float momentum;  // fp32(momentum)
+  int32_t nesterov;
+  int32_t first;   // momentum buffer not yet created (torch: buf = clone(grad))
+};
+
+struct Launch {
+  const Chunk* chunks;  // device chunk table
+  int32_t c0, c1;       // chunk range
+  void* const* ptab;    // device pointer table [DL_MAX_SLOTS][nseg]
+  int32_t nseg;
+  int32_t grid;
+  hipStream_t stream;
+};
+
+hipError_t launch_delta_pack(const Launch& L, int inner_slot, const float* outer, void* wire,
+                             int wire_dtype);
+hipError_t launch_unpack_avg(const Launch& L, const void* wire, int wire_dtype, int divisor,
+                             int dst_slot, float* dst_packed);
+hipError_t launch_unpack_sgd(const Launch& L, const void* wire, int wire_dtype, int divisor,
+                             float* outer, float* mom, SgdArgs a, int inner_slot);
+hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype);
+hipError_t launch_scatter(const Launch& L, const float* packed, int dst_slot);
+hipError_t launch_serialize(const void* src, int src_dtype, int64_t numel, float m0, float m1,
+                            float* out, hipStream_t s);
+hipError_t launch_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id,
+                             float base, float scale, const float* add, hipStream_t s);
+
+}  // namespace dl

@@ -1,0 +1,145 @@
+/*
+ * diloco_hip.h — C-ABI of libdiloco_hip.so, the MI355X (gfx950) implementation of the DiLoCo
+ * outer-step pseudo-gradient sync of mikasenghaas/diloco-swarm.
+ *
+ * The reference has no native code and no FFI: its hot path is per-parameter torch CPU ops
+ * plus one gloo all_reduce per tensor. Each entry point below names the reference code it
+ * replaces (paths relative to the reference repository root). The Python host layer
+ * (diloco-swarm_amd/diloco_amd) binds these symbols with ctypes; see INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every function returns int: 0 = ok, <0 = DL_E_* argument/state error,
+ *     >0 = the hipError_t passed through. dl_last_error() returns a thread-local message.
+ *   - Pointers are plain device (or pinned host, where stated) addresses; no torch types.
+ *   - Memory handed in is owned by the caller; the library owns only the tree handle's
+ *     device tables (freed by dl_tree_destroy).
+ *   - A "packed" buffer holds the tree's tensors back to back in parameters() order, each
+ *     segment starting at a multiple of DL_ALIGN_ELEMS elements; padding is never written.
+ *   - "bucket" selects one bucket of the plan; DL_ALL_BUCKETS (-1) selects the whole tree.
+ *   - All kernels are stream-ordered on the hipStream_t passed in; nothing synchronises the
+ *     host except dl_tree_bind (once per pointer-set change).
+ */
+#ifndef DILOCO_HIP_H
+#define DILOCO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DL_API __attribute__((visibility("default")))
+
+#define DL_ABI_VERSION 1
+#define DL_ALIGN_ELEMS 64      /* segment start alignment in the packed space: 256 B of fp32 */
+#define DL_CHUNK_ELEMS 4096    /* work unit of every segment walker: 16 KiB of fp32 */
+#define DL_ALL_BUCKETS (-1)
+#define DL_MAX_SLOTS 4         /* per-tensor pointer tables per tree */
+
+/* wire / packed dtypes */
+#define DL_F32 0
+#define DL_BF16 1
+#define DL_F16 2
+
+/* errors (negative); positive codes are hipError_t */
+#define DL_OK 0
+#define DL_E_ARG (-1)
+#define DL_E_STATE (-2)
+#define DL_E_ALIGN (-3)
+
+typedef struct dl_tree_s* dl_tree_t;
+typedef void* dl_stream_t; /* hipStream_t */
+
+/* ---- planner (host only; needs no GPU) -------------------------------------------------
+ * Replaces the reference's implicit layout: the per-tensor loop over model.parameters()
+ * in src/comm.py:120-123 and src/utils.py:220,225. Input: numel of each tensor in
+ * parameters() order. Output: seg_off[n+1] (element offsets, each start aligned to
+ * align_elems), bkt_bounds[n_bkt+1] (segment indices; greedy split at tensor boundaries so
+ * a bucket's padded size stays <= cap_elems unless a single tensor exceeds it; cap_elems<=0
+ * = one bucket). bkt_bounds must hold n+1 entries. Bit-exact contract with
+ * oracle/diloco_oracle.c:or_plan_tables. */
+DL_API int dl_plan_tables(const int64_t* numel, int32_t n, int64_t cap_elems, int32_t align_elems,
+                          int64_t* seg_off, int64_t* bkt_bounds, int32_t* n_bkt);
+
+/* ---- tree handle ------------------------------------------------------------------------
+ * One parameter tree on the current device: planner tables + the chunk table + DL_MAX_SLOTS
+ * per-tensor device pointer tables. Created once per model (src/utils.py:213-216
+ * get_outer_model / src/comm.py:81 TrainingComm.__init__ are the natural creation points). */
+DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl_tree_t* out);
+DL_API int dl_tree_destroy(dl_tree_t tree);
+DL_API int dl_tree_query(dl_tree_t tree, int64_t* total_elems, int32_t* n_seg, int32_t* n_bkt,
+                         int32_t* n_chunk);
+DL_API int dl_tree_bucket_range(dl_tree_t tree, int32_t bucket, int64_t* elem_begin,
+                                int64_t* elem_end);
+DL_API int dl_tree_seg_off(dl_tree_t tree, int64_t* seg_off /* n_seg+1 */);
+/* Upload the device addresses of the n_seg tensors of one slot (e.g. inner params, grads).
+ * fp32 tensors, contiguous; a 16-B-misaligned address takes the scalar path. Synchronises
+ * `stream` once (pointer sets change rarely; call again only when addresses change). */
+DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, int32_t n,
+                        dl_stream_t stream);
+/* Cap the grid of every walker launch (0 = default: 8 workgroups per CU). */
+DL_API int dl_tree_set_grid(dl_tree_t tree, int32_t max_blocks);
+
+/* ---- hot-path kernels ----------------------------------------------------------------- */
+
+/* a2: compute_pseudo_gradient, src/utils.py:218-221:
+ *   wire[k] = outer_packed[k] - inner[seg][j]      (fp32 subtract; bf16 wire rounds RNE)
+ * outer_packed: fp32 packed θ_outer; inner: slot `inner_slot`. 12 B/param (fp32 wire). */
+DL_API int dl_delta_pack(dl_tree_t tree, int32_t bucket, int32_t inner_slot,
+                         const float* outer_packed, void* wire, int32_t wire_dtype,
+                         dl_stream_t stream);
+
+/* a3 unpack: src/comm.py:122-123 `param.grad /= num_peers` after the SUM all-reduce:
+ *   dst[seg][j] = wire[k] / divisor   (IEEE true division; divisor 1 = plain copy)
+ * dst is slot `dst_slot` (per-tensor fp32) or, when dst_slot < 0, the packed fp32 buffer
+ * dst_packed (may alias an fp32 wire). 8 B/param. */
+DL_API int dl_unpack_avg(dl_tree_t tree, int32_t bucket, const void* wire, int32_t wire_dtype,
+                         int32_t divisor, int32_t dst_slot, float* dst_packed,
+                         dl_stream_t stream);
+
+/* a3+a4+a5 fused: unpack the summed wire, average, outer SGD (torch.optim.SGD
+ * _single_tensor_sgd as built by src/utils.py:62-63 and stepped at src/train.py:267),
+ * then sync_inner_model (src/utils.py:223-226):
+ *   g = wire/divisor; buf = first ? g : (buf*m) + g; u = nesterov ? fma(buf,m,g) : buf
+ *   θ = fma(u, -lr, θ); inner[seg][j] = θ      (momentum==0: θ = fma(g,-lr,θ), no buf)
+ * inner_slot < 0 skips the inner write. 24 B/param (20 on the first step). */
+DL_API int dl_unpack_sgd(dl_tree_t tree, int32_t bucket, const void* wire, int32_t wire_dtype,
+                         int32_t divisor, float* outer_packed, float* mom_packed, float lr,
+                         float momentum, int32_t nesterov, int32_t first_step,
+                         int32_t inner_slot, dl_stream_t stream);
+
+/* Gather per-tensor fp32 (slot) into a packed buffer of dtype `dtype` (fp32 or bf16).
+ * Used to pack device gradients (DP sync, src/comm.py:117-123 with device grads, called at
+ * src/train.py:251) and to initialise the device θ_outer mirror (src/utils.py:215). */
+DL_API int dl_gather(dl_tree_t tree, int32_t bucket, int32_t src_slot, void* packed,
+                     int32_t dtype, dl_stream_t stream);
+
+/* a5: sync_inner_model, src/utils.py:223-226: dst[seg][j] = packed[k] (fp32). */
+DL_API int dl_scatter(dl_tree_t tree, int32_t bucket, const float* packed, int32_t dst_slot,
+                      dl_stream_t stream);
+
+/* ---- serializer (src/serializer.py:11-15) ----------------------------------------------
+ * out is fp32 of 2*numel elements: out[0] = meta0, out[1] = meta1, out[numel + i] =
+ * float(src[i]) for src dtype DL_F32/DL_BF16/DL_F16. out[2..numel) is left unwritten, as
+ * the reference leaves it uninitialised (torch.empty, src/serializer.py:12). numel >= 2. */
+DL_API int dl_serialize(const void* src, int32_t src_dtype, int64_t numel, float meta0,
+                        float meta1, float* out, dl_stream_t stream);
+
+/* ---- synthetic parameter trees (bench / tests) ------------------------------------------
+ * dst[i] = base + u(seed, stream_id, i) * scale (+ add[i] if add != NULL), with
+ * u = ((splitmix64(seed*0xD1B54A32D192ED03 + (stream_id<<40) + i) >> 40) - 2^23) * 2^-23,
+ * all fp32 ops correctly rounded: bit-identical to diloco_amd.synth (numpy). */
+DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id, float base,
+                         float scale, const float* add, dl_stream_t stream);
+
+/* ---- host memory for the host-resident outer copy (src/utils.py:216) ------------------ */
+DL_API int dl_host_register(void* ptr, int64_t bytes);
+DL_API int dl_host_unregister(void* ptr);
+
+DL_API const char* dl_last_error(void);
+DL_API int dl_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DILOCO_HIP_H */

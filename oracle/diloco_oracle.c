@@ -1,0 +1,118 @@
+/*
+ * diloco_oracle.c -- CPU restatement of the reference's DiLoCo outer step (checker only).
+ *
+ * TEST INFRASTRUCTURE. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may
+ * load this library, and only as the checker; the product path (libdiloco_hip.so) never
+ * links or calls it. Pinned against outputs of the reference itself, imported in the build
+ * container (tests/golden/make_golden.py -> tests/golden/*), see DESIGN.md "Oracle".
+ *
+ * Reference semantics restated (paths relative to the reference repo root):
+ *   or_delta      src/utils.py:218-221   grad = outer - inner                  (1 rounding)
+ *   or_sum_avg    src/comm.py:117-123    all_reduce(SUM) then grad /= num_peers (true div);
+ *                                        num_peers == 1 returns early (no division)
+ *   or_sgd        torch.optim.SGD._single_tensor_sgd as built by src/utils.py:62-63
+ *                 (weight_decay 0, dampening 0, maximize False), stepped at src/train.py:267:
+ *                   first step: buf = clone(g)    else: buf = buf*m (mul_) then + g (add_)
+ *                   nesterov:   u = g + m*buf  -> torch CPU `add(alpha)` is fmadd: fmaf(buf,m,g)
+ *                   param.add_(u, alpha=-lr)   -> fmaf(u, -lr, θ)
+ *                 momentum == 0: θ = fmaf(g, -lr, θ) (no buffer)
+ *   or_copy       src/utils.py:223-226   inner = outer
+ *   or_plan_tables  the build's packed layout (no reference counterpart: the reference walks
+ *                 model.parameters() in order, src/comm.py:120); rule frozen in DESIGN.md.
+ * Build: make -C oracle  (gcc, -O2 -ffp-contract=off so only the fmaf calls fuse).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#define OR_API __attribute__((visibility("default")))
+
+OR_API int or_plan_tables(const int64_t* numel, int32_t n, int64_t cap, int32_t align,
+                          int64_t* seg_off, int64_t* bounds, int32_t* n_bkt) {
+  if (n < 0 || align <= 0) return -1;
+  seg_off[0] = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if (numel[i] < 0) return -1;
+    int64_t end = seg_off[i] + numel[i];
+    seg_off[i + 1] = (end + align - 1) / align * align;
+  }
+  if (n == 0) {
+    bounds[0] = 0;
+    *n_bkt = 0;
+    return 0;
+  }
+  int32_t nb = 0;
+  bounds[0] = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    int64_t start = bounds[nb];
+    if (cap > 0 && i > start && seg_off[i + 1] - seg_off[start] > cap) bounds[++nb] = i;
+  }
+  bounds[++nb] = n;
+  *n_bkt = nb;
+  return 0;
+}
+
+OR_API void or_delta(const float* outer, const float* inner, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = outer[i] - inner[i];
+}
+
+/* out = (((g0 + g1) + g2) + ...) / nranks  (rank-order sum; gloo's order is an
+ * implementation detail of gloo, bit-identical to this only for nranks <= 2). */
+OR_API void or_sum_avg(const float* const* grads, int32_t nranks, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    float s = grads[0][i];
+    for (int32_t r = 1; r < nranks; ++r) s = s + grads[r][i];
+    out[i] = nranks == 1 ? s : s / (float)nranks;
+  }
+}
+
+OR_API void or_sgd(float* theta, float* buf, const float* g, int64_t n, float lr, float momentum,
+                   int32_t nesterov, int32_t first) {
+  const float neg_lr = -lr;
+  for (int64_t i = 0; i < n; ++i) {
+    if (momentum == 0.0f) {
+      theta[i] = fmaf(g[i], neg_lr, theta[i]);
+      continue;
+    }
+    float b = first ? g[i] : (buf[i] * momentum) + g[i];
+    buf[i] = b;
+    float u = nesterov ? fmaf(b, momentum, g[i]) : b;
+    theta[i] = fmaf(u, neg_lr, theta[i]);
+  }
+}
+
+OR_API void or_copy(const float* src, float* dst, int64_t n) { memcpy(dst, src, (size_t)n * 4); }
+
+/* fp32 -> bf16 (round to nearest even, NaN kept NaN) -> fp32: the bf16 wire codec. */
+OR_API void or_bf16_round(const float* x, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t u;
+    memcpy(&u, &x[i], 4);
+    uint32_t r;
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu))
+      r = (u | 0x00400000u) & 0xffff0000u;
+    else
+      r = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+    memcpy(&out[i], &r, 4);
+  }
+}
+
+static uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* Same generator as diloco_amd.synth / dl_fill_synth (cross-checks both). */
+OR_API void or_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream, float base,
+                          float scale, const float* add) {
+  const uint64_t key0 = seed * 0xD1B54A32D192ED03ull + (stream << 40);
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t z = splitmix64(key0 + (uint64_t)i);
+    float u = (float)((int32_t)(z >> 40) - 8388608) * 1.1920928955078125e-07f;
+    float x = base + u * scale;
+    if (add) x = x + add[i];
+    dst[i] = x;
+  }
+}

@@ -1,0 +1,89 @@
+"""The C-ABI library loads without a GPU, exports every symbol include/diloco_hip.h declares,
+its host-only planner matches the frozen tables, and GPU entry points fail loudly here."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, load_json
+from diloco_amd import _lib
+from diloco_amd.plan import plan_tables
+from diloco_amd.trees import get_tree
+
+HEADER = os.path.join(REPO, "include", "diloco_hip.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"DL_API\s+[\w\s\*]+?\b(dl_\w+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    syms = declared_symbols()
+    assert "dl_delta_pack" in syms and "dl_unpack_sgd" in syms and len(syms) >= 19
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    assert sorted(_lib.SIGNATURES) == declared_symbols()
+    assert lib.dl_abi_version() == _lib.ABI_VERSION
+
+
+def test_header_constants_match_python_mirror():
+    src = open(HEADER).read()
+    consts = dict(re.findall(r"#define (DL_\w+) \(?(-?\d+)\)?", src))
+    assert int(consts["DL_ALIGN_ELEMS"]) == _lib.ALIGN_ELEMS
+    assert int(consts["DL_CHUNK_ELEMS"]) == _lib.CHUNK_ELEMS
+    assert int(consts["DL_MAX_SLOTS"]) == _lib.MAX_SLOTS
+    assert int(consts["DL_ABI_VERSION"]) == _lib.ABI_VERSION
+
+
+def test_c_planner_matches_frozen_tables():
+    ref = load_json("plan_tables.json")
+    for name in ("micro", "tiny", "t125", "t1.3b"):
+        numels = get_tree(name).numels()
+        for p in ref[name]["plans"]:
+            seg, bnd = plan_tables(numels, p["cap"], p["align"])
+            assert seg.tolist() == p["seg_off"], name
+            assert bnd.tolist() == p["bkt_bounds"], name
+    for e in ref["edge"]:
+        seg, bnd = plan_tables(e["numels"], e["cap"], e["align"])
+        assert seg.tolist() == e["seg_off"] and bnd.tolist() == e["bkt_bounds"], e
+
+
+def test_planner_properties_t13b():
+    numels = get_tree("t1.3b").numels()
+    seg, bnd = plan_tables(numels, 64 << 20)
+    assert (seg % 64 == 0).all() and (np.diff(seg) >= np.asarray(numels)).all()
+    assert (np.diff(seg) - np.asarray(numels) < 64).all()
+    assert bnd[0] == 0 and bnd[-1] == len(numels) and (np.diff(bnd) > 0).all()
+    for b in range(len(bnd) - 1):
+        size = seg[bnd[b + 1]] - seg[bnd[b]]
+        assert size <= 64 << 20 or bnd[b + 1] - bnd[b] == 1
+
+
+def test_planner_rejects_bad_arguments():
+    with pytest.raises(_lib.DilocoHipError):
+        plan_tables([1, -2, 3])
+    with pytest.raises(_lib.DilocoHipError):
+        plan_tables([1], 0, 0)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_device_entry_points_fail_loudly_without_gpu():
+    from diloco_amd.plan import PackedTree
+
+    with pytest.raises(_lib.DilocoHipError) as e:
+        PackedTree([10, 20])
+    assert "hip" in str(e.value).lower()
+
+
+def test_missing_library_is_an_import_error(tmp_path, monkeypatch):
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(ImportError, match="no CPU fallback"):
+        _lib.load()

@@ -1,0 +1,249 @@
+"""Parity of the HIP path (through the C-ABI) against the reference's outputs and the oracle.
+
+Bit-exact wherever the reference is deterministic: n = 1 and n = 2 (an all-reduce of two
+values is order-free), every per-rank delta, the copy-back and the integer tables. The n = 2
+all-reduce is emulated on one GPU by summing the two replicas' wire buffers (the RCCL step
+itself is exercised by bench.py at N > 1 and by tests/test_dist_gloo.py on CPU).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_json, load_npz, split
+from diloco_amd import _lib, synth
+from diloco_amd.outer import OuterSync
+from diloco_amd.plan import SLOT_GRAD, SLOT_INNER, PackedTree
+from diloco_amd.trees import get_tree
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float32).tobytes()).hexdigest()
+
+
+def _host(ts):
+    return [t.detach().reshape(-1).cpu().numpy() for t in ts]
+
+
+def _engines(spec, n, wire=torch.float32, cap=None, **kw):
+    """n replicas of one tree on this GPU, θ_0 from synth, as get_outer_model sees it."""
+    theta0 = synth.outer_tree_device(spec, DEV)
+    shapes = [s for _, s in spec.params()]
+    engines, inners = [], []
+    for _ in range(n):
+        inner = [t.clone().view(s) for t, s in zip(theta0, shapes)]
+        extra = {} if cap is None else {"bucket_cap_elems": cap}
+        engines.append(OuterSync(inner, world_size=n, wire_dtype=wire, **extra, **kw))
+        inners.append(inner)
+    return engines, inners
+
+
+def _emulated_step(engines, inners, step, per_bucket=False):
+    """One outer step of n replicas on one GPU; returns each replica's delta (host)."""
+    n = len(engines)
+    for r, (e, inner) in enumerate(zip(engines, inners)):
+        theta = e.unpacked(e.theta)
+        synth.inner_tree_device([t.reshape(-1) for t in theta], step, r,
+                                out=[p.view(-1) for p in inner])
+    buckets = range(engines[0].tree.n_buckets) if per_bucket else [_lib.ALL_BUCKETS]
+    deltas = [None] * n
+    for b in buckets:
+        for e in engines:
+            e.pseudo_gradient(b)
+    for r, e in enumerate(engines):
+        deltas[r] = _host(e.unpacked(e.wire.float()))
+    if n > 1:
+        total = engines[0].wire.clone()
+        for e in engines[1:]:
+            total += e.wire
+        for e in engines:
+            e.wire.copy_(total)
+    for b in buckets:
+        for e in engines:
+            e.apply(b)
+    for e in engines:
+        e.steps_done += 1
+    torch.cuda.synchronize()
+    return deltas
+
+
+def test_fill_synth_matches_numpy():
+    for n, seed, stream in [(1, 42, 0), (4097, 7, 3), (1 << 20, 2001, 291)]:
+        x = torch.empty(n, device=DEV)
+        add = torch.linspace(-1, 1, n, device=DEV)
+        synth.fill_device(x, seed, stream, 0.5, 0.25, add=add)
+        ref = synth.values(seed, stream, n, 0.5, 0.25, add=add.cpu().numpy())
+        assert x.cpu().numpy().tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("per_bucket", [False, True])
+def test_micro_matches_reference_bit_exact(n, per_bucket):
+    spec = get_tree("micro")
+    g = load_npz(f"micro_n{n}.npz")
+    engines, inners = _engines(spec, n, cap=4096 if per_bucket else None)
+    if per_bucket:
+        assert engines[0].tree.n_buckets > 2
+    assert np.concatenate(_host(engines[0].unpacked(engines[0].theta))).tobytes() == g["theta0"].tobytes()
+    for s in (1, 2):
+        deltas = _emulated_step(engines, inners, s, per_bucket)
+        assert np.concatenate(deltas[0]).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        assert np.concatenate(deltas[-1]).tobytes() == g[f"delta_s{s}_rlast"].tobytes()
+        for e, inner in zip(engines, inners):
+            th = np.concatenate(_host(e.unpacked(e.theta)))
+            assert th.tobytes() == g[f"theta_s{s}"].tobytes()
+            assert np.concatenate(_host(e.unpacked(e.mom))).tobytes() == g[f"buf_s{s}"].tobytes()
+            assert np.concatenate(_host(inner)).tobytes() == th.tobytes()  # sync_inner_model
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_tiny_matches_reference_digests(n):
+    spec = get_tree("tiny")
+    ref = load_json("tiny_digests.json")[str(n)]["rank0"]
+    engines, inners = _engines(spec, n)
+    numels = spec.numels()
+    for s in (1, 2):
+        deltas = _emulated_step(engines, inners, s)
+        e = engines[0]
+        got = {f"delta_s{s}": deltas[0], f"theta_s{s}": _host(e.unpacked(e.theta)),
+               f"buf_s{s}": _host(e.unpacked(e.mom))}
+        for key, tensors in got.items():
+            for t, (a, d) in enumerate(zip(tensors, ref[key])):
+                assert _sha(a) == d["sha256"], (key, t)
+
+
+def test_t125_full_size_bit_exact_vs_oracle():
+    """BASELINE config #1 tree at full size, two outer steps, against the C oracle."""
+    spec = get_tree("t125")
+    engines, inners = _engines(spec, 1)
+    e = engines[0]
+    st = oracle.OuterState(_host(e.unpacked(e.theta)))
+    for s in (1, 2):
+        _emulated_step(engines, inners, s)
+        inner_host = [synth.values(synth.noise_seed(s, 0), t, x.size, 0.0, synth.NOISE_SCALE, add=x)
+                      for t, x in enumerate(st.theta)]
+        st.step([inner_host])
+        got = _host(e.unpacked(e.theta))
+        for t in range(len(got)):
+            assert got[t].tobytes() == st.theta[t].tobytes(), t
+        mom = _host(e.unpacked(e.mom))
+        for t in range(len(mom)):
+            assert mom[t].tobytes() == st.buf[t].tobytes(), t
+
+
+RAGGED = [1, 3, 5, 4097, 0, 64, 65, 12345, 8191, 4096 * 3 + 7, 2]
+
+
+@pytest.mark.parametrize("momentum,nesterov", [(0.9, True), (0.9, False), (0.0, False)])
+@pytest.mark.parametrize("misaligned", [False, True])
+def test_ragged_tree_and_misaligned_params(momentum, nesterov, misaligned):
+    """Tails, empty tensors, 4-B-aligned (not 16-B) parameter storage -> scalar path."""
+    g0 = torch.Generator().manual_seed(3)
+    host = [torch.randn(n, generator=g0) for n in RAGGED]
+    if misaligned:
+        base = torch.empty(sum(RAGGED) + len(RAGGED), device=DEV)
+        params, o = [], 1
+        for h in host:
+            params.append(base[o:o + h.numel()])
+            o += h.numel() + 1
+        for p, h in zip(params, host):
+            p.copy_(h)
+    else:
+        params = [h.to(DEV) for h in host]
+    e = OuterSync(params, lr=0.7, momentum=momentum, nesterov=nesterov, world_size=1,
+                  bucket_cap_elems=5000)
+    st = oracle.OuterState([h.numpy() for h in host], lr=0.7, momentum=momentum, nesterov=nesterov)
+    for s in (1, 2, 3):
+        noise = [torch.randn(n, generator=g0) * 1e-3 for n in RAGGED]
+        inner_host = [(np.asarray(t) + z.numpy()).astype(np.float32) for t, z in zip(st.theta, noise)]
+        for p, x in zip(params, inner_host):
+            p.copy_(torch.from_numpy(x))
+        deltas, _ = st.step([inner_host])
+        for b in range(e.tree.n_buckets):
+            e.pseudo_gradient(b)
+        wire = _host(e.unpacked(e.wire))
+        for b in range(e.tree.n_buckets):
+            e.apply(b)
+        e.steps_done += 1
+        torch.cuda.synchronize()
+        for t in range(len(RAGGED)):
+            assert wire[t].tobytes() == deltas[0][t].tobytes(), (s, t)
+            assert _host([params[t]])[0].tobytes() == st.theta[t].tobytes(), (s, t)
+        # padding of every packed buffer stays zero
+        mask = torch.ones(e.tree.total, dtype=torch.bool, device=DEV)
+        for t, n in enumerate(RAGGED):
+            lo = int(e.tree.seg_off[t])
+            mask[lo:lo + n] = False
+        assert not e.theta[mask].any() and not e.wire[mask].any()
+
+
+def test_bf16_wire_rounds_like_torch():
+    spec = get_tree("micro")
+    engines, inners = _engines(spec, 1, wire=torch.bfloat16)
+    f32, f32_inners = _engines(spec, 1)
+    for s in (1, 2):
+        e = engines[0]
+        d_bf = _emulated_step(engines, inners, s)[0]
+        d_32 = _emulated_step(f32, f32_inners, s)[0]
+        for a, b in zip(d_bf, d_32):
+            ref = torch.from_numpy(b).to(torch.bfloat16).float().numpy() if s == 1 else None
+            if ref is not None:
+                assert a.tobytes() == ref.tobytes()
+    # bf16 wire error vs the fp32 path is bounded by bf16 resolution of the deltas
+    th_bf = np.concatenate(_host(engines[0].unpacked(engines[0].theta)))
+    th_32 = np.concatenate(_host(f32[0].unpacked(f32[0].theta)))
+    assert np.abs(th_bf - th_32).max() <= 0.7 * 2 * 1e-3 * 2 ** -7 * 3
+
+
+def test_unpack_avg_gather_scatter_roundtrip():
+    numels = RAGGED
+    g0 = torch.Generator().manual_seed(11)
+    grads = [torch.randn(n, generator=g0).to(DEV) for n in numels]
+    dst = [torch.empty(n, device=DEV) for n in numels]
+    tree = PackedTree(numels, 6000)
+    s = torch.cuda.current_stream().cuda_stream
+    tree.bind(SLOT_GRAD, grads, s)
+    tree.bind(SLOT_INNER, dst, s)
+    packed = torch.zeros(tree.total, device=DEV)
+    for b in range(tree.n_buckets):
+        _lib.call("dl_gather", tree.handle, b, SLOT_GRAD, packed.data_ptr(), _lib.DL_F32, s)
+    for div in (1, 3, 8):
+        for b in range(tree.n_buckets):
+            _lib.call("dl_unpack_avg", tree.handle, b, packed.data_ptr(), _lib.DL_F32, div,
+                      SLOT_INNER, None, s)
+        torch.cuda.synchronize()
+        for g, d in zip(grads, dst):
+            ref = g.cpu() if div == 1 else g.cpu() / div
+            assert d.cpu().numpy().tobytes() == ref.numpy().tobytes()
+    # packed -> packed average in place, then scatter back
+    _lib.call("dl_unpack_avg", tree.handle, _lib.ALL_BUCKETS, packed.data_ptr(), _lib.DL_F32, 2,
+              -1, packed.data_ptr(), s)
+    _lib.call("dl_scatter", tree.handle, _lib.ALL_BUCKETS, packed.data_ptr(), SLOT_INNER, s)
+    torch.cuda.synchronize()
+    for g, d in zip(grads, dst):
+        assert d.cpu().numpy().tobytes() == (g.cpu() / 2).numpy().tobytes()
+    tree.close()
+
+
+def test_kernel_argument_errors_are_raised():
+    tree = PackedTree([10, 20])
+    s = torch.cuda.current_stream().cuda_stream
+    buf = torch.zeros(tree.total, device=DEV)
+    with pytest.raises(_lib.DilocoHipError, match="not bound"):
+        _lib.call("dl_delta_pack", tree.handle, -1, SLOT_INNER, buf.data_ptr(), buf.data_ptr(),
+                  _lib.DL_F32, s)
+    with pytest.raises(_lib.DilocoHipError, match="bucket"):
+        _lib.call("dl_scatter", tree.handle, 5, buf.data_ptr(), SLOT_INNER, s)
+    params = [torch.zeros(10, device=DEV), torch.zeros(20, device=DEV)]
+    tree.bind(SLOT_INNER, params, s)
+    with pytest.raises(_lib.DilocoHipError, match="aligned"):
+        _lib.call("dl_gather", tree.handle, -1, SLOT_INNER, buf.data_ptr() + 4, _lib.DL_F32, s)
+    with pytest.raises(_lib.DilocoHipError, match="divisor"):
+        _lib.call("dl_unpack_avg", tree.handle, -1, buf.data_ptr(), _lib.DL_F32, 0, SLOT_INNER,
+                  None, s)
+    tree.close()
