@@ -66,39 +66,30 @@ def build(spec, dev, rank, wire, cap):
     return eng
 
 
-class PhaseTimer:
-    """HIP events on the stream the kernels are launched on (torch's current stream)."""
-
-    def __init__(self):
-        self.events = []
-
-    def mark(self, name):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        self.events.append((name, e))
-
-    def durations(self):
-        out = {}
-        for (n0, e0), (_n1, e1) in zip(self.events, self.events[1:]):
-            if n0 == "end":
-                continue
-            out.setdefault(n0, []).append(e0.elapsed_time(e1))
-        return {k: sum(v) / len(v) for k, v in out.items()}
+def timed_launches(fn, reps):
+    """Average ms per launch of `fn` over `reps` back-to-back launches, HIP events on the
+    current stream (the stream every dl_* kernel is launched on)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
 
 
 def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap):
     eng = build(spec, dev, rank, wire, cap)
     P = spec.total()
-    for _ in range(warmup):
+    for _ in range(max(warmup, 1)):  # >= 1: the timed steps run the steady-state SGD mode
         eng.step()
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timer = PhaseTimer()
     t0 = time.perf_counter()
     for _ in range(steps):
-        eng.step(mark=timer.mark)
+        eng.step()
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -108,51 +99,65 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap):
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    phases = timer.durations()
     wbytes = 2 if wire == torch.bfloat16 else 4
+    # per-kernel average durations: the same kernels on the same buffers, back to back
+    reps = max(steps, 10)
+    kern_ms = {
+        "delta_pack": timed_launches(eng.pseudo_gradient, reps),
+        "unpack_sgd": timed_launches(eng.apply, reps),
+    }
+    kern_bytes = {
+        "delta_pack": (4 + 4 + wbytes) * P,             # read θ, inner; write wire
+        "unpack_sgd": (wbytes + 4 + 4 + 4 + 4 + 4) * P,  # read wire, θ, buf; write θ, buf, inner
+    }
+    kernels = {}
+    for k, b in kern_bytes.items():
+        ms = kern_ms[k]
+        ach = b / (ms * 1e-3) / 1e9
+        kernels[k] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                      "bytes_per_launch": b, "avg_ms": round(ms, 5)}
     res = {
         "tree": spec.name, "params": P, "tensors": len(spec.params()),
         "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
         "ms_per_step": dt / steps * 1e3,
         "value": ws * 4.0 * P / (dt / steps) / 1e9,
-        "phase_ms": phases,
+        "kernels": kernels,
     }
     if ws == 1:
-        kern = {
-            "delta_pack": (4 + 4 + wbytes) * P,             # read θ, inner; write wire
-            "unpack_sgd": (wbytes + 4 + 4 + 4 + 4 + 4) * P,  # read wire, θ, buf; write θ, buf, inner
-        }
-        rl = {}
-        for k, b in kern.items():
-            ms = phases[k]
-            ach = b / (ms * 1e-3) / 1e9
-            rl[k] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                     "bytes_per_launch": b, "avg_ms": round(ms, 5)}
-        dom = max(rl, key=lambda k: rl[k]["avg_ms"])
-        res["roofline"] = dict(rl[dom], kernel=dom)
-        res["kernels"] = rl
+        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+        res["roofline"] = dict(kernels[dom], kernel=dom)
     else:
-        bus = 2.0 * (ws - 1) / ws * wbytes * P
-        ms = phases.get("pipeline", dt / steps * 1e3)
-        ach = bus / (ms * 1e-3) / 1e9
+        # the exchange: every bucket's all-reduce back to back (RCCL over xGMI)
+        def allreduce_all():
+            for b in range(eng.tree.n_buckets):
+                eng.all_reduce(b, async_op=False)
+        if ws > 1:
+            dist.barrier()
+        ar_ms = timed_launches(allreduce_all, max(3, steps // 2))
+        t = torch.tensor([ar_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ar_ms = float(t.item())
+        bus = 2.0 * (ws - 1) / ws * wbytes * eng.tree.total
+        ach = bus / (ar_ms * 1e-3) / 1e9
         peak = (ws - 1) * XGMI_LINK_GBS
         res["roofline"] = {"bound": "xgmi", "achieved": round(ach, 1), "peak": peak,
                            "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None,
-                           "kernel": "rccl_allreduce (pipelined step)", "bus_bytes_per_step": bus}
+                           "kernel": "rccl all_reduce (all buckets)", "avg_ms": round(ar_ms, 4),
+                           "bus_bytes_per_step": bus}
     eng.close()
     del eng
     torch.cuda.empty_cache()
     return res
 
 
-def cpu_baseline(spec, seconds_budget=20.0):
+def cpu_baseline(spec, seconds_budget=12.0):
     """The reference's per-tensor CPU sequence (oracle/torch_restatement.py), 1 thread."""
     sys.path.insert(0, HERE)
     from oracle.torch_restatement import time_steps
 
     numels = spec.numels()
-    t = time_steps(numels, steps=2, threads=1)
+    t, n = time_steps(numels, steps=2, threads=1, budget_s=seconds_budget)
     model = ""
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -163,7 +168,7 @@ def cpu_baseline(spec, seconds_budget=20.0):
     return {
         "value": round(4.0 * spec.total() / t / 1e9, 4), "unit": "GB/s", "cores": 1,
         "kind": "port",
-        "sample": (f"{spec.name} full tree ({spec.total()} params), 2 timed outer steps after 1 "
+        "sample": (f"{spec.name} full tree ({spec.total()} params), {n} timed outer steps after 1 "
                    f"warm step, per-tensor torch CPU restatement of src/utils.py:218-226 + "
                    f"torch SGD-Nesterov (sync_gradients is a no-op at n=1), 1 thread; "
                    f"{t:.3f} s/step"),
@@ -224,8 +229,7 @@ def main():
             },
             "roofline": main_res["roofline"],
             "cpu_baseline": cpu,
-            "kernels": main_res.get("kernels"),
-            "phase_ms": main_res["phase_ms"],
+            "kernels": main_res["kernels"],
             "extra": extra or None,
             "host": platform.node(),
         }

@@ -70,7 +70,8 @@ struct dl_tree_s {
   uint64_t* h_stage = nullptr;  // pinned staging for pointer-table uploads
   std::vector<uint8_t> bound;   // slot bound?
   std::vector<uint8_t> slot_aligned;
-  int32_t grid = 0;
+  int32_t grid = 0;                 // 0 = one workgroup per chunk
+  int32_t flags = DL_TUNE_AUTO;
 };
 
 extern "C" {
@@ -133,11 +134,6 @@ DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl
   t->slot_aligned.assign(DL_MAX_SLOTS, 1);
 
   hipError_t e = hipGetDevice(&t->device);
-  if (e == hipSuccess) {
-    int cus = 0;
-    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device);
-    t->grid = (cus > 0 ? cus : 256) * 8;
-  }
   const size_t cbytes = (t->chunks.empty() ? 1 : t->chunks.size()) * sizeof(dl::Chunk);
   const size_t pbytes = size_t(DL_MAX_SLOTS) * (t->nseg > 0 ? t->nseg : 1) * sizeof(void*);
   if (e == hipSuccess) e = hipMalloc(&t->d_chunks, cbytes);
@@ -197,17 +193,12 @@ DL_API int dl_tree_bucket_range(dl_tree_t t, int32_t b, int64_t* begin, int64_t*
   return DL_OK;
 }
 
-DL_API int dl_tree_set_grid(dl_tree_t t, int32_t max_blocks) {
-  if (!t || max_blocks < 0) return fail(DL_E_ARG, "dl_tree_set_grid: bad argument");
-  if (max_blocks == 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device) !=
-        hipSuccess)
-      cus = 256;
-    t->grid = cus * 8;
-  } else {
-    t->grid = max_blocks;
-  }
+DL_API int dl_tree_tune(dl_tree_t t, int32_t max_blocks, int32_t flags) {
+  if (!t || max_blocks < 0) return fail(DL_E_ARG, "dl_tree_tune: bad argument");
+  if (flags != DL_TUNE_AUTO && (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES)))
+    return fail(DL_E_ARG, "dl_tree_tune: unknown flags 0x%x", flags);
+  t->grid = max_blocks;
+  t->flags = flags;
   return DL_OK;
 }
 
@@ -243,7 +234,13 @@ DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t
 
 namespace {
 
-int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who) {
+// per-kernel launch policy under DL_TUNE_AUTO (tools/sweep.py on T125 / T1.3B)
+constexpr int32_t kAutoDelta = DL_TUNE_NT_LOADS;
+constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
+constexpr int32_t kAutoOther = DL_TUNE_NT_LOADS;
+
+int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who,
+                int32_t auto_flags = kAutoOther) {
   if (!t) return fail(DL_E_ARG, "%s: null tree", who);
   const int32_t nb = int32_t(t->bounds.size()) - 1;
   if (b == DL_ALL_BUCKETS) {
@@ -258,7 +255,8 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
   L->chunks = t->d_chunks;
   L->ptab = t->d_ptab;
   L->nseg = t->nseg;
-  L->grid = t->grid > 0 ? t->grid : 2048;
+  L->grid = t->grid;
+  L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
   L->stream = static_cast<hipStream_t>(s);
   return DL_OK;
 }
@@ -294,7 +292,7 @@ extern "C" {
 DL_API int dl_delta_pack(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,
                          void* wire, int32_t wire_dtype, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack"));
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack", kAutoDelta));
   DL_TRY(check_slot(t, inner_slot, "dl_delta_pack"));
   DL_TRY(check_packed(outer, "dl_delta_pack", "outer"));
   DL_TRY(check_packed(wire, "dl_delta_pack", "wire"));
@@ -323,7 +321,7 @@ DL_API int dl_unpack_sgd(dl_tree_t t, int32_t b, const void* wire, int32_t wire_
                          int32_t nesterov, int32_t first_step, int32_t inner_slot,
                          dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd"));
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd", kAutoUnpackSgd));
   DL_TRY(check_packed(wire, "dl_unpack_sgd", "wire"));
   DL_TRY(check_dtype(wire_dtype, "dl_unpack_sgd"));
   DL_TRY(check_packed(outer, "dl_unpack_sgd", "outer"));

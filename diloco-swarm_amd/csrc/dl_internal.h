@@ -36,7 +36,8 @@ struct Launch {
   int32_t c0, c1;       // chunk range
   void* const* ptab;    // device pointer table [DL_MAX_SLOTS][nseg]
   int32_t nseg;
-  int32_t grid;
+  int32_t grid;   // 0 = one workgroup per chunk
+  int32_t flags;  // DL_TUNE_*
   hipStream_t stream;
 };
 

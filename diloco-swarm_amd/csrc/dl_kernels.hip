@@ -4,8 +4,9 @@
 // 16 KiB chunk of one tensor from the chunk table (a wave-uniform scalar load), issues all of
 // its 16-B loads for the chunk up front (4 float4 per lane per stream), then computes and
 // stores. There are no MFMA and no LDS: the work is elementwise and HBM-bound (DESIGN.md
-// "Kernels"), so what matters is full-width coalesced access and enough bytes in flight
-// (grid-stride over chunks with up to 8 workgroups per CU = 32 waves/CU).
+// "Kernels"), so what matters is full-width coalesced access and enough bytes in flight.
+// Default launch: one workgroup per chunk (T125: 30,458 workgroups, ~119 per CU) with
+// non-temporal loads -- the fastest shape measured (tools/hbm_bench.hip).
 //
 // Numerics follow the reference exactly (compiled with -ffp-contract=off and correctly
 // rounded fp32 division):
@@ -39,39 +40,79 @@ struct bf16_t {
   uint16_t bits;
 };
 
+// Streaming memory ops. NT = non-temporal (`global_load/store_dwordx4 ... nt`): the operands
+// are touched once per outer step and are larger than the 256 MiB Infinity Cache, so keeping
+// them out of the caches measured +10-15 % on streaming loads (tools/hbm_bench.hip,
+// DESIGN.md "Kernels"). Whether stores are NT is a per-tree tuning flag (dl_tree_tune).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// Pointers from the device pointer table are generic (flat) to the compiler; casting to the
+// global address space turns flat_load/store (counted on vmcnt AND lgkmcnt, completed out of
+// order) into global_load/store.
+#define DL_GLOBAL __attribute__((address_space(1)))
+typedef DL_GLOBAL const f32x4* gcf4;
+typedef DL_GLOBAL f32x4* gf4;
+typedef DL_GLOBAL const uint64_t* gcu64;
+typedef DL_GLOBAL uint64_t* gu64;
+
+template <bool NT>
+__device__ __forceinline__ float4 ldf4(const float* p, int v) {
+  gcf4 q = (gcf4)(p) + v;
+  f32x4 r;
+  if constexpr (NT) r = __builtin_nontemporal_load(q);
+  else r = *q;
+  return make_float4(r.x, r.y, r.z, r.w);
+}
+template <bool NT>
+__device__ __forceinline__ void stf4(float* p, int v, float4 x) {
+  gf4 q = (gf4)(p) + v;
+  const f32x4 r = {x.x, x.y, x.z, x.w};
+  if constexpr (NT) __builtin_nontemporal_store(r, q);
+  else *q = r;
+}
+template <bool NT>
+__device__ __forceinline__ uint64_t ld8(const void* p, int v) {
+  gcu64 q = (gcu64)(p) + v;
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void st8(void* p, int v, uint64_t x) {
+  gu64 q = (gu64)(p) + v;
+  if constexpr (NT) __builtin_nontemporal_store(x, q);
+  else *q = x;
+}
+
 template <typename W>
 struct WireIO;
 
 template <>
 struct WireIO<float> {
-  static __device__ __forceinline__ float4 ld4(const float* p, int v) {
-    return reinterpret_cast<const float4*>(p)[v];
-  }
-  static __device__ __forceinline__ void st4(float* p, int v, float4 x) {
-    reinterpret_cast<float4*>(p)[v] = x;
-  }
+  template <bool NT>
+  static __device__ __forceinline__ float4 ld4(const float* p, int v) { return ldf4<NT>(p, v); }
+  template <bool NT>
+  static __device__ __forceinline__ void st4(float* p, int v, float4 x) { stf4<NT>(p, v, x); }
   static __device__ __forceinline__ float ld1(const float* p, int i) { return p[i]; }
   static __device__ __forceinline__ void st1(float* p, int i, float x) { p[i] = x; }
 };
 
 template <>
 struct WireIO<bf16_t> {
+  template <bool NT>
   static __device__ __forceinline__ float4 ld4(const bf16_t* p, int v) {
-    const uint2 r = reinterpret_cast<const uint2*>(p)[v];
-    return make_float4(bf2f(uint16_t(r.x & 0xffffu)), bf2f(uint16_t(r.x >> 16)),
-                       bf2f(uint16_t(r.y & 0xffffu)), bf2f(uint16_t(r.y >> 16)));
+    const uint64_t r = ld8<NT>(p, v);
+    return make_float4(bf2f(uint16_t(r)), bf2f(uint16_t(r >> 16)), bf2f(uint16_t(r >> 32)),
+                       bf2f(uint16_t(r >> 48)));
   }
+  template <bool NT>
   static __device__ __forceinline__ void st4(bf16_t* p, int v, float4 x) {
-    uint2 r;
-    r.x = uint32_t(f2bf(x.x)) | (uint32_t(f2bf(x.y)) << 16);
-    r.y = uint32_t(f2bf(x.z)) | (uint32_t(f2bf(x.w)) << 16);
-    reinterpret_cast<uint2*>(p)[v] = r;
+    const uint64_t r = uint64_t(f2bf(x.x)) | (uint64_t(f2bf(x.y)) << 16) |
+                       (uint64_t(f2bf(x.z)) << 32) | (uint64_t(f2bf(x.w)) << 48);
+    st8<NT>(p, v, r);
   }
   static __device__ __forceinline__ float ld1(const bf16_t* p, int i) { return bf2f(p[i].bits); }
   static __device__ __forceinline__ void st1(bf16_t* p, int i, float x) { p[i].bits = f2bf(x); }
 };
 
-using F32 = WireIO<float>;
 
 __device__ __forceinline__ float4 sub4(float4 a, float4 b) {
   return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
@@ -86,13 +127,14 @@ __device__ __forceinline__ T* slot_ptr(void* const* ptab, int nseg, int slot, co
 }
 
 // ---- the walker ----------------------------------------------------------------------------
-template <class Body>
+// Body::operator() is instantiated per (NTL, NTS) policy: non-temporal loads / stores.
+template <class Body, bool NTL, bool NTS>
 __global__ void __launch_bounds__(kThreads)
     k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ ptab,
            int32_t nseg, Body body) {
   for (int32_t c = c0 + int32_t(blockIdx.x); c < c1; c += int32_t(gridDim.x)) {
     const Chunk ck = chunks[c];
-    body(ck, ptab, nseg, int(threadIdx.x));
+    body.template run<NTL, NTS>(ck, ptab, nseg, int(threadIdx.x));
   }
 }
 
@@ -102,8 +144,8 @@ struct DeltaPack {
   int inner_slot;
   const float* outer;
   W* wire;
-  __device__ __forceinline__ void operator()(const Chunk& ck, void* const* ptab, int nseg,
-                                             int tid) const {
+  template <bool NTL, bool NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
     const float* in = slot_ptr<const float>(ptab, nseg, inner_slot, ck);
     const float* th = outer + ck.poff;
     W* w = wire + ck.poff;
@@ -114,14 +156,14 @@ struct DeltaPack {
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
         if (v < nv) {
-          a[u] = F32::ld4(th, v);
-          b[u] = F32::ld4(in, v);
+          a[u] = ldf4<NTL>(th, v);
+          b[u] = ldf4<NTL>(in, v);
         }
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) WireIO<W>::st4(w, v, sub4(a[u], b[u]));
+        if (v < nv) WireIO<W>::template st4<NTS>(w, v, sub4(a[u], b[u]));
       }
       const int i = (nv << 2) + tid;
       if (i < ck.len) WireIO<W>::st1(w, i, th[i] - in[i]);
@@ -138,8 +180,8 @@ struct UnpackAvg {
   int dst_slot;
   float* dst_packed;
   float d;
-  __device__ __forceinline__ void operator()(const Chunk& ck, void* const* ptab, int nseg,
-                                             int tid) const {
+  template <bool NTL, bool NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
     float* dst = dst_slot >= 0 ? slot_ptr<float>(ptab, nseg, dst_slot, ck) : dst_packed + ck.poff;
     const W* w = wire + ck.poff;
     if (aligned16(dst)) {
@@ -148,12 +190,12 @@ struct UnpackAvg {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) x[u] = WireIO<W>::ld4(w, v);
+        if (v < nv) x[u] = WireIO<W>::template ld4<NTL>(w, v);
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) F32::st4(dst, v, DIV ? div4(x[u], d) : x[u]);
+        if (v < nv) stf4<NTS>(dst, v, DIV ? div4(x[u], d) : x[u]);
       }
       const int i = (nv << 2) + tid;
       if (i < ck.len) {
@@ -171,7 +213,7 @@ struct UnpackAvg {
 
 // a3+a4+a5 fused. MODE 0: momentum 0; 1: first step (buf = g); 2: buf = buf*m + g.
 template <int MODE>
-__device__ __forceinline__ float sgd1(float g, float& buf, float& th, const SgdArgs& a) {
+__device__ __forceinline__ void sgd1(float g, float& buf, float& th, const SgdArgs& a) {
   if (MODE == 0) {
     th = __builtin_fmaf(g, a.neg_lr, th);
   } else {
@@ -179,7 +221,6 @@ __device__ __forceinline__ float sgd1(float g, float& buf, float& th, const SgdA
     const float u = a.nesterov ? __builtin_fmaf(buf, a.momentum, g) : buf;
     th = __builtin_fmaf(u, a.neg_lr, th);
   }
-  return th;
 }
 
 template <typename W, bool DIV, int MODE>
@@ -190,8 +231,8 @@ struct UnpackSgd {
   float d;
   SgdArgs a;
   int inner_slot;
-  __device__ __forceinline__ void operator()(const Chunk& ck, void* const* ptab, int nseg,
-                                             int tid) const {
+  template <bool NTL, bool NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
     float* in = inner_slot >= 0 ? slot_ptr<float>(ptab, nseg, inner_slot, ck) : nullptr;
     const W* w = wire + ck.poff;
     float* th = outer + ck.poff;
@@ -203,23 +244,23 @@ struct UnpackSgd {
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
         if (v < nv) {
-          g[u] = WireIO<W>::ld4(w, v);
-          t[u] = F32::ld4(th, v);
-          if (MODE == 2) m[u] = F32::ld4(mb, v);
+          g[u] = WireIO<W>::template ld4<NTL>(w, v);
+          t[u] = ldf4<NTL>(th, v);
+          if (MODE == 2) m[u] = ldf4<NTL>(mb, v);
         }
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
         if (v < nv) {
-          float4 gg = DIV ? div4(g[u], d) : g[u];
+          const float4 gg = DIV ? div4(g[u], d) : g[u];
           sgd1<MODE>(gg.x, m[u].x, t[u].x, a);
           sgd1<MODE>(gg.y, m[u].y, t[u].y, a);
           sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
           sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
-          F32::st4(th, v, t[u]);
-          if (MODE != 0) F32::st4(mb, v, m[u]);
-          if (in) F32::st4(in, v, t[u]);
+          stf4<NTS>(th, v, t[u]);
+          if (MODE != 0) stf4<NTS>(mb, v, m[u]);
+          if (in) stf4<NTS>(in, v, t[u]);
         }
       }
       const int i = (nv << 2) + tid;
@@ -251,8 +292,8 @@ template <typename W>
 struct Gather {
   int src_slot;
   W* packed;
-  __device__ __forceinline__ void operator()(const Chunk& ck, void* const* ptab, int nseg,
-                                             int tid) const {
+  template <bool NTL, bool NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
     const float* src = slot_ptr<const float>(ptab, nseg, src_slot, ck);
     W* p = packed + ck.poff;
     if (aligned16(src)) {
@@ -261,12 +302,12 @@ struct Gather {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) x[u] = F32::ld4(src, v);
+        if (v < nv) x[u] = ldf4<NTL>(src, v);
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) WireIO<W>::st4(p, v, x[u]);
+        if (v < nv) WireIO<W>::template st4<NTS>(p, v, x[u]);
       }
       const int i = (nv << 2) + tid;
       if (i < ck.len) WireIO<W>::st1(p, i, src[i]);
@@ -280,8 +321,8 @@ struct Gather {
 struct Scatter {
   const float* packed;
   int dst_slot;
-  __device__ __forceinline__ void operator()(const Chunk& ck, void* const* ptab, int nseg,
-                                             int tid) const {
+  template <bool NTL, bool NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
     float* dst = slot_ptr<float>(ptab, nseg, dst_slot, ck);
     const float* p = packed + ck.poff;
     if (aligned16(dst)) {
@@ -290,12 +331,12 @@ struct Scatter {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) x[u] = F32::ld4(p, v);
+        if (v < nv) x[u] = ldf4<NTL>(p, v);
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) F32::st4(dst, v, x[u]);
+        if (v < nv) stf4<NTS>(dst, v, x[u]);
       }
       const int i = (nv << 2) + tid;
       if (i < ck.len) dst[i] = p[i];
@@ -305,14 +346,23 @@ struct Scatter {
   }
 };
 
+template <class Body, bool NTL, bool NTS>
+hipError_t run_policy(const Launch& L, const Body& body, int32_t grid) {
+  hipLaunchKernelGGL((k_walk<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream, L.chunks,
+                     L.c0, L.c1, L.ptab, L.nseg, body);
+  return hipGetLastError();
+}
+
 template <class Body>
 hipError_t run(const Launch& L, const Body& body) {
   const int32_t n = L.c1 - L.c0;
   if (n <= 0) return hipSuccess;
-  const int32_t grid = n < L.grid ? n : L.grid;
-  hipLaunchKernelGGL(k_walk<Body>, dim3(grid), dim3(kThreads), 0, L.stream, L.chunks, L.c0, L.c1,
-                     L.ptab, L.nseg, body);
-  return hipGetLastError();
+  const int32_t grid = (L.grid > 0 && L.grid < n) ? L.grid : n;  // default: one workgroup per chunk
+  const bool ntl = (L.flags & DL_TUNE_NT_LOADS) != 0, nts = (L.flags & DL_TUNE_NT_STORES) != 0;
+  if (ntl && nts) return run_policy<Body, true, true>(L, body, grid);
+  if (ntl) return run_policy<Body, true, false>(L, body, grid);
+  if (nts) return run_policy<Body, false, true>(L, body, grid);
+  return run_policy<Body, false, false>(L, body, grid);
 }
 
 // ---- serializer and synthetic fill -----------------------------------------------------------

@@ -21,6 +21,8 @@ CHUNK_ELEMS = 4096
 ALL_BUCKETS = -1
 MAX_SLOTS = 4
 DL_F32, DL_BF16, DL_F16 = 0, 1, 2
+TUNE_NT_LOADS, TUNE_NT_STORES = 1, 2
+TUNE_AUTO = -1
 
 _i32, _i64, _u64, _f32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
 _vp = ctypes.c_void_p
@@ -37,7 +39,7 @@ SIGNATURES = {
     "dl_tree_bucket_range": (ctypes.c_int, [_vp, _i32, _pi64, _pi64]),
     "dl_tree_seg_off": (ctypes.c_int, [_vp, _pi64]),
     "dl_tree_bind": (ctypes.c_int, [_vp, _i32, _pu64, _i32, _vp]),
-    "dl_tree_set_grid": (ctypes.c_int, [_vp, _i32]),
+    "dl_tree_tune": (ctypes.c_int, [_vp, _i32, _i32]),
     "dl_delta_pack": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _vp]),
     "dl_unpack_avg": (ctypes.c_int, [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp]),
     "dl_unpack_sgd": (
@@ -81,6 +83,11 @@ def load() -> ctypes.CDLL:
                 "`make -C diloco-swarm_amd/csrc` (hipcc --offload-arch=gfx950). "
                 "There is no CPU fallback for the DiLoCo outer-step path."
             )
+        # PyTorch-ROCm bundles its own HIP runtime (torch/lib/libamdhip64.so, soname
+        # libamdhip64.so.7). Import torch first so our NEEDED libamdhip64.so.7 binds to that
+        # already-loaded runtime: one HIP runtime per process, shared streams and pointers.
+        import torch  # noqa: F401
+
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

@@ -79,6 +79,9 @@ class PackedTree:
 
         No-op when the addresses are unchanged since the last bind of this slot.
         """
+        key = tuple([t.data_ptr() for t in tensors])
+        if self._bound[slot] == key:  # fast path: same storage as last time (every outer step)
+            return
         ptrs = []
         for i, t in enumerate(tensors):
             if t.dtype.itemsize != 4 or not t.is_floating_point():
@@ -90,17 +93,15 @@ class PackedTree:
             ptrs.append(t.data_ptr())
         if len(ptrs) != self.n_seg:
             raise ValueError(f"{len(ptrs)} tensors for a {self.n_seg}-tensor tree")
-        key = tuple(ptrs)
-        if self._bound[slot] == key:
-            return
         arr = np.asarray(ptrs, dtype=np.uint64)
         _lib.call("dl_tree_bind", self.handle, slot,
                   arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if ptrs else None,
                   len(ptrs), stream)
         self._bound[slot] = key
 
-    def set_grid(self, max_blocks: int) -> None:
-        _lib.call("dl_tree_set_grid", self.handle, int(max_blocks))
+    def tune(self, max_blocks: int = 0, flags: int = _lib.TUNE_AUTO) -> None:
+        """Launch shape of the walker kernels (speed only; results are identical)."""
+        _lib.call("dl_tree_tune", self.handle, int(max_blocks), int(flags))
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:

@@ -37,8 +37,11 @@ class TorchOuterStep:
             pi.data.copy_(po.detach())
 
 
-def time_steps(numels, steps=2, threads=1, seed=0):
-    """Seconds per outer step of the per-tensor torch CPU path on a tree of `numels`."""
+def time_steps(numels, steps=2, threads=1, seed=0, budget_s=None):
+    """Seconds per outer step of the per-tensor torch CPU path on a tree of `numels`.
+
+    With budget_s, keeps stepping (at least `steps` times) until budget_s seconds elapsed.
+    Returns (seconds_per_step, steps_timed)."""
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(seed)
     inner = [torch.empty(n).uniform_(-0.03, 0.03, generator=g) for n in numels]
@@ -47,6 +50,8 @@ def time_steps(numels, steps=2, threads=1, seed=0):
         t.add_(torch.empty_like(t).uniform_(-1e-3, 1e-3, generator=g))
     st.step()  # first step allocates the momentum buffers (not timed)
     t0 = time.perf_counter()
-    for _ in range(steps):
+    done = 0
+    while done < steps or (budget_s is not None and time.perf_counter() - t0 < budget_s):
         st.step()
-    return (time.perf_counter() - t0) / steps
+        done += 1
+    return (time.perf_counter() - t0) / done, done

@@ -36,6 +36,7 @@ def test_library_exports_every_declared_symbol():
 def test_header_constants_match_python_mirror():
     src = open(HEADER).read()
     consts = dict(re.findall(r"#define (DL_\w+) \(?(-?\d+)\)?", src))
+    assert int(consts["DL_TUNE_AUTO"]) == _lib.TUNE_AUTO
     assert int(consts["DL_ALIGN_ELEMS"]) == _lib.ALIGN_ELEMS
     assert int(consts["DL_CHUNK_ELEMS"]) == _lib.CHUNK_ELEMS
     assert int(consts["DL_MAX_SLOTS"]) == _lib.MAX_SLOTS
