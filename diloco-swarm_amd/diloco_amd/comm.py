@@ -1,0 +1,245 @@
+"""Drop-in for src/comm.py: TrainingComm / InferenceComm with the DP sync on RCCL + HIP.
+
+`TrainingComm(world, shape, logger)` keeps the reference's constructor and methods
+(src/comm.py:71-149). What changes is `sync_gradients(model)` (src/comm.py:117-123):
+
+  reference:  for p in model.parameters(): all_reduce(p.grad, SUM, gloo); p.grad /= n
+  here:       one bucketed pass on the GPU over an RCCL group of the same ranks
+              - host gradients (the DiLoCo outer model, src/train.py:265): the outer model's
+                device mirror all-reduces its packed wire and divides in HBM
+                (mirror.HostOuterMirror.all_reduce), then writes the averages back to .grad
+              - device gradients (plain DP / SWARM, src/train.py:251): gradsync.GradSync
+                (dl_gather -> RCCL -> dl_unpack_avg)
+  Unchanged semantics: no-op for a single peer (no zero-fill either, src/comm.py:118-119),
+  missing gradients become zeros, true division by the peer count, averages on every rank.
+
+The pipeline point-to-point threads (src/comm.py:16-69) keep the reference's gloo transport
+and queue protocol; their framing uses the HIP Serializer. They are outside the outer-step
+path and carried for interface completeness.
+"""
+from __future__ import annotations
+
+import os
+import random
+import threading
+import time
+from queue import Queue
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .gradsync import GradSync
+from .serializer import Metadata, Serializer
+
+
+class SendThread:
+    """Queue-fed sender (src/comm.py:16-38): optional framing, then dist.send from host memory."""
+
+    TIMEOUT = 1e-4
+
+    def __init__(self, shape: Tuple[int, ...], group, tag: int = 0, serialize: bool = True,
+                 start: bool = True, **kwargs):
+        self.shape, self.group, self.tag, self.serialize = shape, group, tag, serialize
+        self.logger = kwargs.get("logger")
+        self.queue: Queue = Queue()
+        if serialize:
+            self.serializer = Serializer(shape)
+            self.shape = self.serializer.shape
+        if start:
+            threading.Thread(target=self._send_loop, daemon=True).start()
+
+    def send(self, dst: int, tensor: torch.Tensor, metadata: Optional[Metadata]) -> None:
+        self.queue.put((dst, tensor, metadata))
+
+    def _send_loop(self):
+        while True:
+            if self.queue.empty():
+                time.sleep(self.TIMEOUT)
+                continue
+            dst, tensor, metadata = self.queue.get()
+            if self.serialize:
+                tensor = self.serializer.serialize(tensor, metadata)
+            dist.send(tensor.to("cpu"), dst=dst, group=self.group, tag=self.tag)
+
+
+class RecvThread:
+    """Receiver thread (src/comm.py:40-69): dist.recv into host memory, optional unframing."""
+
+    def __init__(self, shape: Tuple[int, ...], group, tag: int = 0, requires_grad: bool = True,
+                 dtype: torch.dtype = torch.float32, serialize: bool = True, start: bool = True,
+                 **kwargs):
+        self.shape, self.group, self.tag = shape, group, tag
+        self.requires_grad, self.dtype, self.serialize = requires_grad, dtype, serialize
+        self.logger = kwargs.get("logger")
+        self.queue: Queue = Queue()
+        if serialize:
+            self.serializer = Serializer(shape)
+            self.shape = self.serializer.shape
+        if start:
+            threading.Thread(target=self._recv_loop, daemon=True).start()
+
+    @property
+    def can_receive(self) -> bool:
+        return not self.queue.empty()
+
+    def load(self, tensor: Optional[torch.Tensor], metadata: Optional[Metadata]) -> None:
+        self.queue.put((-1, tensor, metadata))
+
+    def receive(self):
+        return self.queue.get()
+
+    def _recv_loop(self):
+        while True:
+            buf = torch.empty(self.shape, dtype=self.dtype, requires_grad=self.requires_grad)
+            src = dist.recv(buf, group=self.group, tag=self.tag)
+            meta = None
+            if self.serialize:
+                buf, meta = self.serializer.deserialize(buf)
+            self.queue.put((src, buf, meta))
+
+
+# Collective backend of the DP group for device tensors: "nccl" = RCCL over xGMI (the
+# product). "gloo" exists for multi-process tests that share one GPU (RCCL refuses two ranks
+# on one device); the kernels are the same HIP kernels either way.
+DP_BACKEND = os.environ.get("DILOCO_DP_BACKEND", "nccl")
+
+
+class TrainingComm:
+    def __init__(self, world, shape: Tuple[int, ...], logger):
+        self.world, self.shape, self.logger = world, shape, logger
+        kw = {"tag": 0, "serialize": True, "requires_grad": True, "logger": logger}
+        self.forward_send_thread = SendThread(shape, group=world.next_stage_group,
+                                              start=world.has_next_stage, **kw)
+        self.backward_recv_thread = RecvThread(shape, group=world.next_stage_group,
+                                               start=world.has_next_stage, **kw)
+        self.backward_send_thread = SendThread(shape, group=world.prev_stage_group,
+                                               start=world.has_prev_stage, **kw)
+        self.forward_recv_thread = RecvThread(shape, group=world.prev_stage_group,
+                                              start=world.has_prev_stage, **kw)
+        self._rccl_group = None
+        self._grad_syncs: Dict[int, GradSync] = {}
+
+    # ---- pipeline p2p (unchanged protocol) ----------------------------------------------
+    def send_forward(self, tensor: torch.Tensor, metadata: Metadata) -> None:
+        if not self.world.has_next_stage:
+            return
+        dst = random.choice(self.world.stage2ranks[self.world.stage + 1])
+        self.forward_send_thread.send(dst=dst, tensor=tensor, metadata=metadata)
+
+    def send_backward(self, dst: int, tensor: torch.Tensor, metadata: Metadata) -> None:
+        if not self.world.has_prev_stage:
+            return
+        self.backward_send_thread.send(dst=dst, tensor=tensor, metadata=metadata)
+
+    def recv_forward(self):
+        return self.forward_recv_thread.receive()
+
+    def recv_backward(self):
+        return self.backward_recv_thread.receive()
+
+    def load_forward(self, metadata: Metadata) -> None:
+        self.forward_recv_thread.load(tensor=None, metadata=metadata)
+
+    # ---- the DP sync (outer-step hot path) ----------------------------------------------
+    @property
+    def num_peers(self) -> int:
+        return len(self.world.stage2ranks[self.world.stage])
+
+    def dp_group(self, device: torch.device):
+        """The collective group of this stage's DP ranks on `device`'s transport.
+
+        GPU: an RCCL group over world.stage2ranks[stage], created on first use by exactly the
+        ranks that sync together (like the reference's curr_stage_group, src/world.py:39).
+        CPU tensors use the reference's own gloo group."""
+        if device.type != "cuda":
+            return self.world.curr_stage_group
+        if self._rccl_group is None:
+            self._rccl_group = dist.new_group(self.world.stage2ranks[self.world.stage],
+                                              backend=DP_BACKEND, use_local_synchronization=True)
+        return self._rccl_group
+
+    def sync_gradients(self, model: nn.Module) -> None:
+        num_peers = self.num_peers
+        if num_peers == 1:
+            return
+        params = list(model.parameters())
+        if not params:
+            return
+        if params[0].device.type == "cpu":
+            from .utils import outer_mirror
+
+            m = outer_mirror(model)
+            m.all_reduce(self.dp_group(m.device), num_peers)
+            return
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        gs = self._grad_syncs.get(id(model))
+        if gs is None or not gs.matches(params):
+            gs = GradSync(params, self.dp_group(params[0].device), num_peers)
+            self._grad_syncs[id(model)] = gs
+        gs.sync()
+
+    # ---- metrics aggregation (src/comm.py:125-149) ---------------------------------------
+    def sync_outputs(self, outputs):
+        peers = self.world.stage2ranks[self.world.stage]
+        if len(peers) == 1:
+            return outputs
+        gathered: List = [None] * len(peers)
+        dist.all_gather_object(gathered, outputs, group=self.world.curr_stage_group)
+
+        def total(vals):
+            return sum(v for v in vals if v not in (0, None))
+
+        def mean(vals):
+            kept = [v for v in vals if v not in (0, None)]
+            return sum(kept) / len(kept) if kept else 0
+
+        return type(outputs)(
+            step=outputs.step,
+            tokens=total([o.tokens for o in gathered]),
+            num_micro_batches=total([o.num_micro_batches for o in gathered]),
+            time=mean([o.time for o in gathered]),
+            loss=mean([o.loss for o in gathered]),
+            lr=mean([o.lr for o in gathered]),
+            norm=mean([o.norm for o in gathered]),
+            micro_step_time=mean([o.micro_step_time for o in gathered]),
+        )
+
+
+class InferenceComm:
+    """Leader ring for sampling (src/comm.py:151-183); unframed p2p, unchanged protocol."""
+
+    def __init__(self, world, shape: Tuple[int, ...], logger):
+        self.world, self.shape, self.logger = world, shape, logger
+        kw = {"tag": 1, "serialize": False, "requires_grad": False, "start": True,
+              "logger": logger}
+        if not world.is_leader:
+            return
+        if world.is_first_stage:
+            self.send_thread = SendThread(shape, group=world.next_stage_group, **kw)
+            self.recv_thread = RecvThread(shape[:-1], group=world.first_last_stage_group,
+                                          dtype=torch.long, **kw)
+        elif world.is_last_stage:
+            self.send_thread = SendThread(shape[:-1], group=world.first_last_stage_group, **kw)
+            self.recv_thread = RecvThread(shape, group=world.prev_stage_group, **kw)
+        else:
+            self.send_thread = SendThread(shape, group=world.next_stage_group, **kw)
+            self.recv_thread = RecvThread(shape, group=world.prev_stage_group, **kw)
+        self.receive_tensor_type = "hidden_states" if not world.is_first_stage else "input_ids"
+        self.dst = (world.stage2leader[world.stage + 1] if not world.is_last_stage
+                    else world.stage2leader[0])
+
+    def receive(self):
+        return self.receive_tensor_type, self.recv_thread.receive()[1]
+
+    def send(self, tensor: torch.Tensor) -> None:
+        if self.world.rank == self.dst:
+            self.load(tensor)
+            return
+        self.send_thread.send(dst=self.dst, tensor=tensor, metadata=None)
+
+    def load(self, tensor: torch.Tensor) -> None:
+        self.recv_thread.load(tensor=tensor, metadata=None)

@@ -1,0 +1,91 @@
+"""The kernel backend of the outer-step engines: libdiloco_hip.so through its C-ABI.
+
+Every engine (OuterSync, GradSync, HostOuterMirror) calls these methods and nothing else for
+compute, so the orchestration above them (bucketing, pipelining, /n, optimizer state) is one
+code path. `HipKernels` is the only backend the package ships; it launches on the current
+HIP stream of the tensors' device and raises if the library or the GPU is missing.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from .plan import DEFAULT_BUCKET_CAP_ELEMS, PackedTree
+
+_DT = {torch.float32: _lib.DL_F32, torch.bfloat16: _lib.DL_BF16}
+
+
+def wire_code(dtype: torch.dtype) -> int:
+    try:
+        return _DT[dtype]
+    except KeyError:
+        raise TypeError(f"unsupported packed dtype {dtype} (float32 or bfloat16)") from None
+
+
+def _s(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+class HipKernels:
+    """Segment-walker kernels of libdiloco_hip.so (DESIGN.md "Kernels")."""
+
+    name = "hip"
+
+    def check_device(self, device: torch.device) -> None:
+        if device.type != "cuda":
+            raise ValueError(f"the HIP outer-step kernels need device tensors, got {device}")
+        _lib.load()
+
+    def tree(self, numels: Sequence[int], device: torch.device,
+             cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS) -> PackedTree:
+        self.check_device(device)
+        with torch.cuda.device(device):
+            return PackedTree(numels, cap_elems)
+
+    def bind(self, tree: PackedTree, slot: int, tensors: Sequence[torch.Tensor], device) -> None:
+        tree.bind(slot, tensors, torch.cuda.current_stream(device).cuda_stream)
+
+    def delta_pack(self, tree, bucket, inner_slot, theta, wire) -> None:
+        _lib.call("dl_delta_pack", tree.handle, bucket, inner_slot, theta.data_ptr(),
+                  wire.data_ptr(), wire_code(wire.dtype), _s(theta))
+
+    def unpack_sgd(self, tree, bucket, wire, divisor, theta, mom, lr, momentum, nesterov,
+                   first, inner_slot) -> None:
+        _lib.call("dl_unpack_sgd", tree.handle, bucket, wire.data_ptr(), wire_code(wire.dtype),
+                  int(divisor), theta.data_ptr(), _ptr(mom), float(lr), float(momentum),
+                  int(nesterov), int(first), int(inner_slot), _s(theta))
+
+    def unpack_avg(self, tree, bucket, wire, divisor, dst_slot, dst_packed=None) -> None:
+        _lib.call("dl_unpack_avg", tree.handle, bucket, wire.data_ptr(), wire_code(wire.dtype),
+                  int(divisor), int(dst_slot), _ptr(dst_packed), _s(wire))
+
+    def gather(self, tree, bucket, src_slot, packed) -> None:
+        _lib.call("dl_gather", tree.handle, bucket, src_slot, packed.data_ptr(),
+                  wire_code(packed.dtype), _s(packed))
+
+    def scatter(self, tree, bucket, packed, dst_slot) -> None:
+        _lib.call("dl_scatter", tree.handle, bucket, packed.data_ptr(), dst_slot, _s(packed))
+
+
+_DEFAULT = None
+
+
+def default_kernels():
+    """The backend the engines use: HipKernels unless a test installed its own checker
+    backend with set_default_kernels (tests/oracle_kernels.py; never done by the package)."""
+    global _DEFAULT
+    if _DEFAULT is None:
+        _DEFAULT = HipKernels()
+    return _DEFAULT
+
+
+def set_default_kernels(k) -> None:
+    """Test hook: route the engines through `k` (None restores HipKernels)."""
+    global _DEFAULT
+    _DEFAULT = k

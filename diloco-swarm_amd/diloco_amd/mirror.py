@@ -1,0 +1,211 @@
+"""Device mirror of the reference's host-resident outer model.
+
+The reference keeps θ_outer on the CPU (`get_outer_model` -> deepcopy(inner).to("cpu"),
+src/utils.py:213-216) and works on it per tensor with pageable copies. The drop-in functions
+keep that host-visible state exact -- outer params, outer.grad and the optimizer's momentum
+buffers are ordinary CPU tensors holding the reference's values -- but lay them out as views
+into three pinned, packed host arenas and mirror them in HBM:
+
+    host (pinned, packed)        device (HBM, packed)
+    h_theta  <- params' storage   d_theta
+    h_grad   <- .grad views       d_wire   (fp32: the reference's fp32 all-reduce)
+    h_mom    <- momentum views    d_mom
+
+so every host<->device transfer is ONE DMA of the whole arena over PCIe, and the compute is the
+HIP segment-walker kernels. Coherence is tracked with PyTorch's per-tensor version counters:
+a host tensor modified in place by torch code (e.g. the reference's CPU SGD) has a new
+`_version`, and the device copy is re-uploaded before its next use. Writes through `.data`
+bypass version counters; call `invalidate()` after such writes.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .kernels import default_kernels
+from .outer import pipelined_buckets
+from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER
+
+ALL = _lib.ALL_BUCKETS
+
+
+def _check_host_params(params: Sequence[torch.Tensor]) -> None:
+    for i, p in enumerate(params):
+        if p.device.type != "cpu":
+            raise ValueError(f"outer parameter {i} is on {p.device}; the outer copy lives on the "
+                             "host (src/utils.py:216)")
+        if p.dtype != torch.float32:
+            raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
+
+
+class HostOuterMirror:
+    def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
+                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS):
+        self.params: List[torch.nn.Parameter] = list(outer_model.parameters())
+        if not self.params:
+            raise ValueError("outer model has no parameters")
+        _check_host_params(self.params)
+        self.k = kernels or default_kernels()
+        self.device = torch.device(device)
+        self.numels = [p.numel() for p in self.params]
+        self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems)
+        self.offs = [int(o) for o in self.tree.seg_off[:-1]]
+        total = self.tree.total
+        pin = self.device.type == "cuda"
+        self.h_theta = torch.zeros(total, dtype=torch.float32, pin_memory=pin)
+        self.h_grad = torch.zeros(total, dtype=torch.float32, pin_memory=pin)
+        self.h_mom: Optional[torch.Tensor] = None
+        self.d_theta = torch.zeros(total, dtype=torch.float32, device=self.device)
+        self.d_wire = torch.zeros(total, dtype=torch.float32, device=self.device)
+        self.d_mom: Optional[torch.Tensor] = None
+        self._theta_key = None
+        self._grad_key = None
+        self._mom_key = None
+        self._relay_params()
+
+    # ---- host arenas ---------------------------------------------------------------------
+    def _view(self, arena: torch.Tensor, i: int) -> torch.Tensor:
+        o = self.offs[i]
+        return arena[o:o + self.numels[i]].view(self.params[i].shape)
+
+    def _relay_params(self) -> None:
+        """Move every outer parameter's storage into h_theta (values unchanged)."""
+        with torch.no_grad():
+            for i, p in enumerate(self.params):
+                v = self._view(self.h_theta, i)
+                if p.data.data_ptr() != v.data_ptr():
+                    v.copy_(p.data)
+                    p.data = v
+        self._theta_key = None
+
+    def _param_key(self):
+        return tuple((p._version, p.data_ptr()) for p in self.params)
+
+    def _grad_key_now(self):
+        return tuple(None if p.grad is None else (p.grad.data_ptr(), p.grad._version)
+                     for p in self.params)
+
+    def _stream_sync(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def invalidate(self) -> None:
+        """Forget every device copy (after host writes that bypass version counters)."""
+        self._theta_key = self._grad_key = self._mom_key = None
+
+    # ---- coherence ------------------------------------------------------------------------
+    def theta_to_device(self) -> None:
+        if any(p.data_ptr() != self._view(self.h_theta, i).data_ptr()
+               for i, p in enumerate(self.params)):
+            self._relay_params()
+        key = self._param_key()
+        if key != self._theta_key:
+            self.d_theta.copy_(self.h_theta, non_blocking=True)
+            self._theta_key = key
+
+    def _set_grad_views(self) -> None:
+        for i, p in enumerate(self.params):
+            v = self._view(self.h_grad, i)
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+
+    def grads_to_device(self, zero_fill_missing: bool) -> None:
+        """Make d_wire equal the host gradients (missing ones per the caller's rule)."""
+        if self._grad_key is not None and self._grad_key == self._grad_key_now():
+            return
+        with torch.no_grad():
+            for i, p in enumerate(self.params):
+                v = self._view(self.h_grad, i)
+                if p.grad is None:
+                    if not zero_fill_missing:
+                        raise RuntimeError(
+                            f"outer parameter {i} has no gradient: the fused outer step updates "
+                            "every tensor (call compute_pseudo_gradient first)")
+                    v.zero_()  # src/comm.py:121: zeros_like(param)
+                elif p.grad.data_ptr() != v.data_ptr():
+                    v.copy_(p.grad)
+        self._set_grad_views()
+        self.d_wire.copy_(self.h_grad, non_blocking=True)
+        self._grad_key = self._grad_key_now()
+
+    def _grads_to_host(self) -> None:
+        self.h_grad.copy_(self.d_wire, non_blocking=True)
+        self._set_grad_views()
+        self._stream_sync()
+        self._grad_key = self._grad_key_now()
+
+    # ---- the four reference operations --------------------------------------------------
+    def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
+        """outer.grad = outer - inner (src/utils.py:218-221), delta computed in HBM."""
+        self.theta_to_device()
+        self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
+        self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
+        self._grads_to_host()
+
+    def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
+        """grad = Σ_peers grad / n (src/comm.py:120-123): RCCL on d_wire, /n in HBM."""
+        self.grads_to_device(zero_fill_missing=True)
+
+        def view(b):
+            lo, hi = self.tree.bucket_ranges[b]
+            return self.d_wire[lo:hi]
+
+        pipelined_buckets(
+            self.tree.n_buckets, lambda b: None,
+            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
+            lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
+        )
+        self._grads_to_host()
+
+    def sgd_step(self, lr: float, momentum: float, nesterov: bool,
+                 host_bufs: Optional[List[Optional[torch.Tensor]]]) -> List[Optional[torch.Tensor]]:
+        """torch.optim.SGD._single_tensor_sgd over the whole tree (src/train.py:267).
+
+        host_bufs: the optimizer's current momentum buffers (None = not created yet, i.e.
+        the first step). Returns the momentum buffers to store in the optimizer state
+        (views of the pinned h_mom arena)."""
+        self.theta_to_device()
+        self.grads_to_device(zero_fill_missing=False)
+        first = True
+        if momentum != 0:
+            if self.h_mom is None:
+                pin = self.device.type == "cuda"
+                self.h_mom = torch.zeros_like(self.h_theta, pin_memory=pin)
+                self.d_mom = torch.zeros_like(self.d_theta)
+            have = [b is not None for b in host_bufs]
+            if any(have) and not all(have):
+                raise RuntimeError("momentum buffers exist for some outer parameters only")
+            first = not any(have)
+            if not first:
+                views = [self._view(self.h_mom, i) for i in range(len(self.params))]
+                key = tuple((b.data_ptr(), b._version) for b in host_bufs)
+                if key != self._mom_key:
+                    with torch.no_grad():
+                        for b, v in zip(host_bufs, views):
+                            if b.data_ptr() != v.data_ptr():
+                                v.copy_(b)
+                    self.d_mom.copy_(self.h_mom, non_blocking=True)
+        self.k.unpack_sgd(self.tree, ALL, self.d_wire, 1, self.d_theta,
+                          self.d_mom if momentum != 0 else None, lr, momentum, nesterov, first, -1)
+        self.h_theta.copy_(self.d_theta, non_blocking=True)
+        bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
+        if momentum != 0:
+            self.h_mom.copy_(self.d_mom, non_blocking=True)
+            bufs = [self._view(self.h_mom, i) for i in range(len(self.params))]
+        self._stream_sync()
+        self._theta_key = self._param_key()  # arena writes do not bump parameter versions
+        if momentum != 0:
+            self._mom_key = tuple((b.data_ptr(), b._version) for b in bufs)
+        return bufs
+
+    def copy_to_inner(self, inner_params: Sequence[torch.Tensor]) -> None:
+        """inner = outer (src/utils.py:223-226), scattered from HBM."""
+        self.theta_to_device()
+        self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
+        self.k.scatter(self.tree, ALL, self.d_theta, SLOT_INNER)
+
+    def close(self) -> None:
+        self.tree.close()

@@ -22,13 +22,30 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER, PackedTree
+from .kernels import default_kernels
+from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER
 
-_WIRE = {torch.float32: _lib.DL_F32, torch.bfloat16: _lib.DL_BF16}
+ALL = _lib.ALL_BUCKETS
 
 
-def _stream_handle(device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+def pipelined_buckets(n_buckets: int, pack: Callable[[int], None],
+                      reduce: Callable[[int], object], unpack: Callable[[int], None]) -> None:
+    """pack(b) -> async reduce(b) -> wait -> unpack(b), overlapped across buckets.
+
+    Issue order: pack(0) red(0) pack(1) red(1) [wait 0, unpack(0)] pack(2) red(2) [wait 1,
+    unpack(1)] ...: the collective stream always has the next bucket queued behind the
+    current one, while the compute stream packs ahead and unpacks behind it.
+    """
+    works = [None] * n_buckets
+    for b in range(n_buckets):
+        pack(b)
+        works[b] = reduce(b)
+        if b >= 1:
+            works[b - 1].wait()
+            unpack(b - 1)
+    if n_buckets:
+        works[n_buckets - 1].wait()
+        unpack(n_buckets - 1)
 
 
 class OuterSync:
@@ -45,51 +62,42 @@ class OuterSync:
         world_size: Optional[int] = None,
         wire_dtype: torch.dtype = torch.float32,
         bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS,
+        kernels=None,
     ):
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
                                            for p in params]
         if not self.params:
             raise ValueError("OuterSync needs at least one parameter")
-        self.device = self.params[0].device
-        if self.device.type != "cuda":
-            raise ValueError("OuterSync keeps the outer state in HBM: parameters must be on a GPU")
-        if wire_dtype not in _WIRE:
-            raise ValueError(f"wire dtype {wire_dtype} (supported: float32, bfloat16)")
         if nesterov and momentum == 0:
             raise ValueError("Nesterov momentum requires a momentum")  # torch.optim.SGD's check
+        self.k = kernels or default_kernels()
+        self.device = self.params[0].device
         self.lr, self.momentum, self.nesterov = float(lr), float(momentum), bool(nesterov)
         self.wire_dtype = wire_dtype
         self.group = group
         if world_size is None:
             world_size = dist.get_world_size(group) if dist.is_initialized() else 1
         self.world_size = int(world_size)
-        with torch.cuda.device(self.device):
-            self.tree = PackedTree([p.numel() for p in self.params], bucket_cap_elems)
-            s = _stream_handle(self.device)
-            self.tree.bind(SLOT_INNER, self.params, s)
-            # a1 get_outer_model (src/utils.py:213-216): θ_outer starts as a copy of inner.
-            # zeros, so the alignment padding of every packed buffer stays zero forever.
-            self.theta = torch.zeros(self.tree.total, dtype=torch.float32, device=self.device)
-            self.mom = (torch.zeros(self.tree.total, dtype=torch.float32, device=self.device)
-                        if self.momentum != 0 else None)
-            self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, device=self.device)
-            _lib.call("dl_gather", self.tree.handle, _lib.ALL_BUCKETS, SLOT_INNER,
-                      self.theta.data_ptr(), _lib.DL_F32, s)
+        self.tree = self.k.tree([p.numel() for p in self.params], self.device, bucket_cap_elems)
+        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+        # a1 get_outer_model (src/utils.py:213-216): θ_outer starts as a copy of inner.
+        # zeros, so the alignment padding of every packed buffer stays zero forever.
+        z = dict(device=self.device)
+        self.theta = torch.zeros(self.tree.total, dtype=torch.float32, **z)
+        self.mom = (torch.zeros(self.tree.total, dtype=torch.float32, **z)
+                    if self.momentum != 0 else None)
+        self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, **z)
+        self.k.gather(self.tree, ALL, SLOT_INNER, self.theta)
         self.steps_done = 0
 
     # ---- building blocks (each stream-ordered on the current stream) ----------------------
-    def _rebind(self, s: int) -> None:
-        self.tree.bind(SLOT_INNER, self.params, s)
-
-    def pseudo_gradient(self, bucket: int = _lib.ALL_BUCKETS) -> None:
+    def pseudo_gradient(self, bucket: int = ALL) -> None:
         """wire[bucket] = θ_outer - inner (a2)."""
-        s = _stream_handle(self.device)
-        self._rebind(s)
-        _lib.call("dl_delta_pack", self.tree.handle, bucket, SLOT_INNER, self.theta.data_ptr(),
-                  self.wire.data_ptr(), _WIRE[self.wire_dtype], s)
+        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+        self.k.delta_pack(self.tree, bucket, SLOT_INNER, self.theta, self.wire)
 
     def bucket_view(self, bucket: int) -> torch.Tensor:
-        if bucket == _lib.ALL_BUCKETS:
+        if bucket == ALL:
             return self.wire
         lo, hi = self.tree.bucket_ranges[bucket]
         return self.wire[lo:hi]
@@ -99,49 +107,23 @@ class OuterSync:
         return dist.all_reduce(self.bucket_view(bucket), op=dist.ReduceOp.SUM, group=self.group,
                                async_op=async_op)
 
-    def apply(self, bucket: int = _lib.ALL_BUCKETS, write_inner: bool = True) -> None:
+    def apply(self, bucket: int = ALL, write_inner: bool = True) -> None:
         """g = wire/n; Nesterov SGD on θ_outer; inner = θ_outer (a3 /n, a4, a5)."""
-        s = _stream_handle(self.device)
-        _lib.call(
-            "dl_unpack_sgd", self.tree.handle, bucket, self.wire.data_ptr(),
-            _WIRE[self.wire_dtype], self.world_size, self.theta.data_ptr(),
-            self.mom.data_ptr() if self.mom is not None else None,
-            self.lr, self.momentum, int(self.nesterov), int(self.steps_done == 0),
-            SLOT_INNER if write_inner else -1, s,
-        )
+        self.k.unpack_sgd(self.tree, bucket, self.wire, self.world_size, self.theta, self.mom,
+                          self.lr, self.momentum, self.nesterov, self.steps_done == 0,
+                          SLOT_INNER if write_inner else -1)
 
     # ---- the outer step ---------------------------------------------------------------------
-    def step(self, mark: Optional[Callable[[str], None]] = None) -> None:
-        """One DiLoCo outer step over the whole tree (src/train.py:261-269).
-
-        `mark(name)` (optional) is called between phases, e.g. to record HIP events.
-        """
-        m = mark or (lambda _n: None)
+    def step(self) -> None:
+        """One DiLoCo outer step over the whole tree (src/train.py:261-269)."""
         if self.world_size == 1:
             # src/comm.py:118-119: one peer -> no all-reduce and no division
-            m("delta_pack")
-            self.pseudo_gradient(_lib.ALL_BUCKETS)
-            m("unpack_sgd")
-            self.apply(_lib.ALL_BUCKETS)
-            m("end")
+            self.pseudo_gradient(ALL)
+            self.apply(ALL)
         else:
-            nb = self.tree.n_buckets
-            works = [None] * nb
-            m("pipeline")
-            for b in range(nb):
-                self.pseudo_gradient(b)
-                works[b] = self.all_reduce(b, async_op=True)
-                if b >= 1:
-                    works[b - 1].wait()
-                    self.apply(b - 1)
-            works[nb - 1].wait()
-            self.apply(nb - 1)
-            m("end")
+            pipelined_buckets(self.tree.n_buckets, self.pseudo_gradient,
+                              lambda b: self.all_reduce(b, async_op=True), self.apply)
         self.steps_done += 1
-
-    def state_tensors(self):
-        """(θ_outer, momentum) packed views, for checkpoints and tests."""
-        return self.theta, self.mom
 
     def unpacked(self, packed: torch.Tensor) -> List[torch.Tensor]:
         """Per-tensor views into a packed buffer (shapes of the inner params)."""

@@ -1,0 +1,97 @@
+"""Checker backend for CPU tests: the engines' kernel interface implemented with the oracle.
+
+TEST INFRASTRUCTURE. Installed only by tests (diloco_amd.kernels.set_default_kernels) so the
+engines' orchestration -- buckets, pipelining over a real gloo process group, /n, optimizer
+state, host coherence -- runs on CPU tensors at world_size 2 and 4. Every elementwise step is
+the C oracle (oracle/diloco_oracle.c); the packed layout comes from the product's host-only
+planner (dl_plan_tables), whose tables are pinned separately.
+"""
+import numpy as np
+import torch
+
+from diloco_amd.plan import plan_tables
+from oracle import oracle
+
+
+class CpuTree:
+    def __init__(self, numels, cap):
+        self.numels = [int(n) for n in numels]
+        seg, bnd = plan_tables(self.numels, cap)
+        self.seg_off = seg
+        self.bounds = bnd
+        self.total = int(seg[-1])
+        self.n_seg = len(self.numels)
+        self.n_buckets = len(bnd) - 1
+        self.n_chunks = 0
+        self.bucket_ranges = [(int(seg[bnd[b]]), int(seg[bnd[b + 1]])) for b in range(self.n_buckets)]
+        self.slots = {}
+
+    def segs(self, bucket):
+        if bucket == -1:
+            return range(self.n_seg)
+        return range(int(self.bounds[bucket]), int(self.bounds[bucket + 1]))
+
+    def close(self):
+        pass
+
+
+def _np(t):
+    return t.detach().numpy()
+
+
+class OracleKernels:
+    name = "oracle"
+    default_device = torch.device("cpu")
+
+    def check_device(self, device):
+        assert device.type == "cpu"
+
+    def tree(self, numels, device, cap_elems=64 << 20):
+        return CpuTree(numels, cap_elems)
+
+    def bind(self, tree, slot, tensors, device):
+        tree.slots[slot] = [t.detach().reshape(-1) for t in tensors]
+
+    def _seg(self, tree, packed, i):
+        o = int(tree.seg_off[i])
+        return _np(packed)[o:o + tree.numels[i]]
+
+    def delta_pack(self, tree, bucket, inner_slot, theta, wire):
+        assert wire.dtype == torch.float32
+        for i in tree.segs(bucket):
+            d = oracle.delta(np.ascontiguousarray(self._seg(tree, theta, i)),
+                             _np(tree.slots[inner_slot][i]).copy())
+            self._seg(tree, wire, i)[:] = d
+
+    def unpack_sgd(self, tree, bucket, wire, divisor, theta, mom, lr, momentum, nesterov, first,
+                   inner_slot):
+        for i in tree.segs(bucket):
+            g = self._seg(tree, wire, i).copy()
+            if divisor != 1:
+                g = (g / np.float32(divisor)).astype(np.float32)
+            th = self._seg(tree, theta, i).copy()
+            b = self._seg(tree, mom, i).copy() if mom is not None else None
+            oracle.sgd(th, b, g, lr, momentum, nesterov, first)
+            self._seg(tree, theta, i)[:] = th
+            if mom is not None:
+                self._seg(tree, mom, i)[:] = b
+            if inner_slot >= 0:
+                _np(tree.slots[inner_slot][i])[:] = th
+
+    def unpack_avg(self, tree, bucket, wire, divisor, dst_slot, dst_packed=None):
+        for i in tree.segs(bucket):
+            g = self._seg(tree, wire, i).copy()
+            if divisor != 1:
+                g = (g / np.float32(divisor)).astype(np.float32)
+            if dst_slot >= 0:
+                _np(tree.slots[dst_slot][i])[:] = g
+            else:
+                self._seg(tree, dst_packed, i)[:] = g
+
+    def gather(self, tree, bucket, src_slot, packed):
+        for i in tree.segs(bucket):
+            self._seg(tree, packed, i)[:] = _np(tree.slots[src_slot][i])
+
+    def scatter(self, tree, bucket, packed, dst_slot):
+        for i in tree.segs(bucket):
+            _np(tree.slots[dst_slot][i])[:] = self._seg(tree, packed, i)

@@ -1,0 +1,259 @@
+"""The drop-in surface on the GPU: the reference's call sequence of src/train.py:261-269 with
+diloco_amd's get_outer_model / compute_pseudo_gradient / TrainingComm.sync_gradients /
+get_optimizer(...).step() / sync_inner_model, HIP kernels underneath, compared bit-exact with
+the reference's own outputs (tests/golden/micro_n{1,2}.npz).
+
+Two-peer cases run two processes on the one GPU of the box. RCCL refuses two ranks on one
+device, so these use a gloo DP group on the device tensors (DILOCO_DP_BACKEND=gloo); the
+kernels are the product's HIP kernels. The RCCL transport itself runs in bench.py at N > 1.
+"""
+import os
+import socket
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO, load_json, load_npz
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Cfg:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+SGD_CFG = _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True)
+
+
+def _module(values, shapes, device):
+    m = torch.nn.Module()
+    m.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.from_numpy(v.copy()).view(s))
+                                   for v, s in zip(values, shapes)])
+    return m.to(device)
+
+
+def _flat(ts):
+    return np.concatenate([t.detach().cpu().numpy().reshape(-1) for t in ts])
+
+
+def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0):
+    """The reference's outer step sequence with the drop-in functions (this process = DP
+    rank `rank` of `n`; the default process group must exist)."""
+    from diloco_amd import synth
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cpu")
+    outer = get_outer_model(inner)  # src/train.py:382: before the inner model moves
+    inner = inner.to("cuda:0")
+    if stock_sgd:
+        opt = torch.optim.SGD(outer.parameters(), lr=0.7, momentum=0.9, nesterov=True)
+    else:
+        opt = get_optimizer(outer, SGD_CFG)
+        assert type(opt).__name__ == "OuterSGD"
+    comm = TrainingComm(World.from_default_group(1), (1, 1, 32), None)
+    rec = {}
+    for s in range(1, steps + 1):
+        prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
+        vals = synth.inner_tree(prev, s, rank)
+        with torch.no_grad():
+            for p, v in zip(inner.parameters(), vals):
+                p.copy_(torch.from_numpy(v).view(p.shape))
+        compute_pseudo_gradient(inner, outer)
+        rec[f"delta_s{s}"] = _flat(p.grad for p in outer.parameters())
+        comm.sync_gradients(outer)
+        rec[f"avg_s{s}"] = _flat(p.grad for p in outer.parameters())
+        opt.step()
+        rec[f"theta_s{s}"] = _flat(outer.parameters())
+        rec[f"buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"] for p in outer.parameters())
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        rec[f"inner_s{s}"] = _flat(inner.parameters())
+        if host_shift and s == 1:
+            # a host-side in-place update between outer steps must reach the device mirror
+            with torch.no_grad():
+                for p in outer.parameters():
+                    p.add_(host_shift)
+    return rec
+
+
+def _init_single():
+    if not dist.is_initialized():
+        f = tempfile.mktemp(prefix="dl_pg_")
+        dist.init_process_group("gloo", init_method=f"file://{f}", rank=0, world_size=1)
+
+
+@pytest.mark.parametrize("stock_sgd", [False, True])
+def test_dropin_single_peer_matches_reference(stock_sgd):
+    _init_single()
+    g = load_npz("micro_n1.npz")
+    rec = _outer_steps(0, 1, stock_sgd=stock_sgd)
+    for s in (1, 2):
+        assert rec[f"delta_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        assert rec[f"avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()  # n=1: no sync
+        assert rec[f"theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+        assert rec[f"buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes()
+        assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+
+
+def test_dropin_host_writes_are_seen_by_the_device_mirror():
+    """θ_outer changed on the host between outer steps (version counter bump) -> re-upload."""
+    from conftest import split
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from oracle import oracle
+
+    _init_single()
+    g = load_npz("micro_n1.npz")
+    rec = _outer_steps(0, 1, host_shift=0.25)
+    numels = get_tree("micro").numels()
+    st = oracle.OuterState([(t + np.float32(0.25)).astype(np.float32)
+                            for t in split(g["theta_s1"], numels)])
+    st.buf = [b.copy() for b in split(g["buf_s1"], numels)]
+    st.steps = 1
+    st.step([synth.inner_tree(st.theta, 2, 0)])
+    assert rec["theta_s2"].tobytes() == np.concatenate(st.theta).tobytes()
+    assert rec["inner_s2"].tobytes() == np.concatenate(st.theta).tobytes()
+
+
+def test_outer_params_stay_host_tensors_with_reference_layout():
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import compute_pseudo_gradient, get_outer_model
+
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cpu")
+    outer = get_outer_model(inner)
+    inner = inner.to("cuda:0")
+    compute_pseudo_gradient(inner, outer)
+    for p, q in zip(outer.parameters(), inner.parameters()):
+        assert p.device.type == "cpu" and p.grad.device.type == "cpu"
+        assert p.shape == q.shape and p.grad.shape == q.shape
+        assert p.is_pinned()
+
+
+def _worker(rank, world, port, mode, out):
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["DILOCO_DP_BACKEND"] = "gloo"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    rec = {}
+    if mode == "dropin":
+        rec = _outer_steps(rank, world)
+    elif mode == "engine":
+        from diloco_amd import synth
+        from diloco_amd.outer import OuterSync
+        from diloco_amd.trees import get_tree
+
+        spec = get_tree("micro")
+        shapes = [s for _, s in spec.params()]
+        params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+        eng = OuterSync(params, world_size=world, bucket_cap_elems=4096)
+        for s in (1, 2):
+            th = [t.reshape(-1) for t in eng.unpacked(eng.theta)]
+            synth.inner_tree_device(th, s, rank, out=[p.view(-1) for p in params])
+            eng.step()
+            torch.cuda.synchronize()
+            rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
+            rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.mom))
+            rec[f"inner_s{s}"] = _flat(params)
+    elif mode == "dp":
+        from diloco_amd.comm import TrainingComm
+        from diloco_amd.world import World
+
+        g = torch.Generator().manual_seed(100 + rank)
+        m = torch.nn.Module()
+        m.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(n)) for n in
+                                       (1, 3, 5000, 64, 4097, 70000)]).to("cuda:0")
+        for i, p in enumerate(m.parameters()):
+            if i != 1:  # one missing gradient: zero-filled (src/comm.py:121)
+                p.grad = torch.randn(p.numel(), generator=g).to("cuda:0")
+        ref = [p.grad.clone() if p.grad is not None else torch.zeros_like(p)
+               for p in m.parameters()]
+        for r in ref:
+            dist.all_reduce(r, op=dist.ReduceOp.SUM)
+            r /= world
+        TrainingComm(World.from_default_group(1), (1, 1, 4), None).sync_gradients(m)
+        torch.cuda.synchronize()
+        rec["got"] = _flat(p.grad for p in m.parameters())
+        rec["ref"] = _flat(ref)
+    np.savez(os.path.join(out, f"{mode}_r{rank}.npz"), **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(mode, world=2):
+    out = tempfile.mkdtemp(prefix="dl_gpu_")
+    mp.spawn(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True)
+    return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("mode", ["dropin", "engine"])
+def test_two_peers_on_gpu_match_reference(mode):
+    g = load_npz("micro_n2.npz")
+    for rec in _run(mode):
+        for s in (1, 2):
+            assert rec[f"theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
+            assert rec[f"buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes(), (mode, s)
+            assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
+            if mode == "dropin":
+                assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
+
+
+def test_dp_sync_of_device_grads_two_peers():
+    for rec in _run("dp"):
+        assert rec["got"].tobytes() == rec["ref"].tobytes()
+
+
+def test_serializer_matches_reference_fixture():
+    from diloco_amd.serializer import Serializer
+
+    for case in load_json("serializer.json"):
+        dtype = getattr(torch, case["dtype"])
+        x = torch.tensor(case["x"], dtype=torch.float32).to(dtype).view(case["shape"]).cuda()
+        s = Serializer(tuple(case["shape"]))
+        assert list(s.shape) == case["serializer_shape"]
+        y = s.serialize(x, tuple(case["meta"]))
+        assert list(y.shape) == case["out_shape"] and str(y.dtype).split(".")[-1] == case["out_dtype"]
+        assert y[0].flatten()[:2].tolist() == case["meta_plane"]
+        assert y[1].flatten().tolist() == case["payload"]
+        t, m = s.deserialize(y)
+        assert list(t.shape) == case["deser_shape"] and list(m) == case["deser_meta"]
+        assert torch.equal(t, y[1])
+
+
+def test_serializer_errors_and_large_payload():
+    from diloco_amd.serializer import Serializer
+
+    s = Serializer((1,))
+    with pytest.raises(IndexError):
+        s.serialize(torch.ones(1, device="cuda"), (0, 1))
+    with pytest.raises(ValueError):
+        s.serialize(torch.ones(4), (0, 1))
+    x = torch.randn(32, 1024, 768, device="cuda")  # the experiment's (mbs, seq, n_embd)
+    y = Serializer(tuple(x.shape)).serialize(x, (5, 7))
+    assert torch.equal(y[1], x) and y[0].flatten()[:2].tolist() == [5.0, 7.0]
+    xb = torch.randn(3, 1001, device="cuda").to(torch.bfloat16)
+    yb = Serializer((3, 1001)).serialize(xb, (1, 2))
+    assert torch.equal(yb[1], xb.float())
