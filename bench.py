@@ -38,6 +38,19 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0       # per link per direction; busBW peak (n-1)*153
 
 
+def load_pmc(tree):
+    """Per-launch HBM bytes from the committed rocprofv3 counter passes of the same kernels
+    (tools/gpu_pmc.sh -> profiles/rNN_pmc_<tree>.json, FETCH_SIZE x2 gfx950 correction)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_pmc_{tree}.json")))
+    if not files:
+        return {}
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {k: v["hbm_bytes"] for k, v in d.get("kernels", {}).items()}
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -51,7 +64,10 @@ def setup_dist(n_gpus):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if ws > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        from datetime import timedelta
+
+        # a hung collective becomes an error after 5 minutes instead of the 10-minute default
+        dist.init_process_group("nccl", device_id=dev, timeout=timedelta(minutes=5))
     return ws, rank, dev
 
 
@@ -110,12 +126,15 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap):
         "delta_pack": (4 + 4 + wbytes) * P,             # read θ, inner; write wire
         "unpack_sgd": (wbytes + 4 + 4 + 4 + 4 + 4) * P,  # read wire, θ, buf; write θ, buf, inner
     }
+    pmc = load_pmc(spec.name) if wire == torch.float32 else {}
     kernels = {}
     for k, b in kern_bytes.items():
         ms = kern_ms[k]
         ach = b / (ms * 1e-3) / 1e9
+        tr = pmc.get(k)
         kernels[k] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                      "traffic": round(tr) if tr else None,
                       "bytes_per_launch": b, "avg_ms": round(ms, 5)}
     res = {
         "tree": spec.name, "params": P, "tensors": len(spec.params()),
@@ -149,6 +168,104 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap):
     del eng
     torch.cuda.empty_cache()
     return res
+
+
+def parity_check(dev, ws, rank, wire):
+    """The RCCL + HIP path against a plain torch fp32 statement of the same step (tiny tree,
+    many buckets): averaged deltas normwise <= 1e-6 (north-star tolerance) and every replica
+    bit-identical after the full step."""
+    spec = get_tree("tiny")
+    eng = build(spec, dev, rank, wire, 1 << 20)
+    nb = eng.tree.n_buckets
+    for b in range(nb):
+        eng.pseudo_gradient(b)
+        eng.all_reduce(b, async_op=False) if ws > 1 else None
+    got_sum = [t.float().clone() for t in eng.unpacked(eng.wire)]
+    # torch fp32 reference: θ_0 and every rank's inner regenerated locally (counter-based)
+    theta0 = synth.outer_tree_device(spec, dev)
+    acc = [torch.zeros_like(t) for t in theta0]
+    for r in range(ws):
+        inner_r = synth.inner_tree_device(theta0, 1, r)
+        d = [t - i for t, i in zip(theta0, inner_r)]
+        if wire == torch.bfloat16:
+            d = [x.to(torch.bfloat16).float() for x in d]
+        acc = [a + x for a, x in zip(acc, d)]
+    worst = 0.0
+    for g, ref in zip(got_sum, acc):
+        g = g.reshape(-1) / ws
+        ref = ref / ws
+        scale = float(ref.abs().max().clamp_min(1e-30))
+        worst = max(worst, float((g - ref).abs().max()) / scale)
+    for b in range(nb):
+        eng.apply(b)
+    eng.steps_done += 1
+    torch.cuda.synchronize()
+    ck = torch.stack([eng.theta.view(torch.int32).to(torch.int64).sum(),
+                      -eng.theta.view(torch.int32).to(torch.int64).sum()])
+    if ws > 1:
+        dist.all_reduce(ck, op=dist.ReduceOp.MAX)
+    identical = bool(ck[0].item() == -ck[1].item())
+    tol = 1e-6 if wire == torch.float32 else 1e-2
+    eng.close()
+    return {"tree": "tiny", "buckets": nb, "avg_delta_normwise_err": worst, "tolerance": tol,
+            "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
+
+
+def dropin_rate(spec, dev, ws, rank, steps):
+    """The reference's call sequence (src/train.py:261-269) through the drop-in functions:
+    host-resident outer model, PCIe transfers included (DESIGN.md "Host-memory ends")."""
+    from types import SimpleNamespace
+
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+
+    if not dist.is_initialized():
+        import tempfile
+
+        dist.init_process_group("gloo", init_method="file://" + tempfile.mktemp(prefix="dlpg"),
+                                rank=0, world_size=1)
+    shapes = [s for _, s in spec.params()]
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList(
+        [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
+    outer = get_outer_model(inner)
+    opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
+    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
+                            out=[p.data.view(-1) for p in inner.parameters()])
+    phases = {"compute_pseudo_gradient": 0.0, "sync_gradients": 0.0, "outer_step": 0.0,
+              "sync_inner_model": 0.0}
+
+    def one(record):
+        t = [time.perf_counter()]
+        compute_pseudo_gradient(inner, outer)
+        t.append(time.perf_counter())
+        comm.sync_gradients(outer)
+        t.append(time.perf_counter())
+        opt.step()
+        t.append(time.perf_counter())
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        t.append(time.perf_counter())
+        if record:
+            for k, a, b in zip(phases, t, t[1:]):
+                phases[k] += b - a
+
+    one(False)
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one(True)
+    dt = (time.perf_counter() - t0) / steps
+    P = spec.total()
+    return {"tree": spec.name, "value": round(ws * 4.0 * P / dt / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(dt * 1e3, 3),
+            "phase_ms": {k: round(v / steps * 1e3, 3) for k, v in phases.items()},
+            "pcie_bytes_per_step": (16 if ws > 1 else 12) * P,
+            "note": "host outer model; D2H of delta, (avg), θ, momentum per step"}
 
 
 def cpu_baseline(spec, seconds_budget=12.0):
@@ -187,6 +304,7 @@ def main():
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--extra-tree", default="t1.3b", help="second tree measured beside (or 'none')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the host-outer-model rate")
     a = ap.parse_args()
 
     ws, rank, dev = setup_dist(a.gpus)
@@ -201,6 +319,16 @@ def main():
         es = get_tree(a.extra_tree)
         r = run_tree(es, dev, ws, rank, max(3, a.steps // 4), 1, wire, cap)
         extra[es.name] = {k: r[k] for k in ("value", "ms_per_step", "roofline", "buckets", "params")}
+    parity = dropin = None
+    try:
+        parity = parity_check(dev, ws, rank, wire)
+    except Exception as e:  # reported, never hidden
+        parity = {"ok": False, "error": repr(e)}
+    if not a.no_dropin:
+        try:
+            dropin = dropin_rate(spec, dev, ws, rank, 5)
+        except Exception as e:
+            dropin = {"error": repr(e)}
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         log("timing the CPU baseline")
@@ -230,11 +358,13 @@ def main():
             "roofline": main_res["roofline"],
             "cpu_baseline": cpu,
             "kernels": main_res["kernels"],
+            "parity": parity,
+            "dropin_pcie": dropin,
             "extra": extra or None,
             "host": platform.node(),
         }
         print(json.dumps(line), flush=True)
-    if ws > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Launch each hot-path kernel a few times on a tree (for rocprofv3 counter passes)."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "diloco-swarm_amd"))
+
+import torch  # noqa: E402
+
+from diloco_amd import synth  # noqa: E402
+from diloco_amd.outer import OuterSync  # noqa: E402
+from diloco_amd.trees import get_tree  # noqa: E402
+
+
+def main():
+    tree = sys.argv[1] if len(sys.argv) > 1 else "t125"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    dev = torch.device("cuda", 0)
+    spec = get_tree(tree)
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)]
+    eng = OuterSync(params, world_size=1)
+    synth.inner_tree_device([p.view(-1) for p in params], 1, 0, out=[p.view(-1) for p in params])
+    eng.step()
+    for _ in range(reps):
+        eng.pseudo_gradient()
+    for _ in range(reps):
+        eng.apply()
+    torch.cuda.synchronize()
+    print(f"kernel_driver: {tree} x{reps} done")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Per-launch HBM bytes of the outer-step kernels from rocprofv3 --pmc passes.
+
+    python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> \
+        <tree> <out.json>
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports exactly half the bytes
+of a wide coalesced streaming read -> x2. WRITE_SIZE (KiB) is exact for 16-B-per-lane stores.
+Counters are summed over the dimensions rocprofv3 reports per dispatch, then averaged over the
+dispatches of each kernel.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    for k in ("DeltaPack", "UnpackSgd", "UnpackAvg", "Gather", "Scatter", "k_fill_synth"):
+        if k in name:
+            return {"DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd", "UnpackAvg": "unpack_avg",
+                    "Gather": "gather", "Scatter": "scatter", "k_fill_synth": "fill_synth"}[k] + (
+                        "_first" if "UnpackSgd" in name and ", 1>" in name else "")
+    return None
+
+
+def load(path, counter):
+    per = defaultdict(float)  # (kernel, dispatch) -> value
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        k = short(r["Kernel_Name"])
+        if k is None:
+            continue
+        per[(k, r["Dispatch_Id"])] += float(r["Counter_Value"])
+    agg = defaultdict(list)
+    for (k, _d), v in per.items():
+        agg[k].append(v)
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    fpath, wpath, tree, out = sys.argv[1:5]
+    f = load(fpath, "FETCH_SIZE")
+    w = load(wpath, "WRITE_SIZE")
+    res = {"tree": tree, "unit": "bytes per launch", "correction": "FETCH_SIZE x2 (gfx950)",
+           "kernels": {}}
+    for k in sorted(set(f) | set(w)):
+        fb = f.get(k, 0.0) * 1024 * 2
+        wb = w.get(k, 0.0) * 1024
+        res["kernels"][k] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
