@@ -9,19 +9,22 @@ One step = one full outer step of src/train.py:261-269 over the whole synthetic 
 rank, device-resident (θ_outer, momentum and the wire buffer live in HBM):
     dl_delta_pack (wire = θ_outer - inner) -> [RCCL all_reduce(SUM) per bucket, pipelined]
     -> dl_unpack_sgd (g = wire/n, Nesterov SGD, inner = θ_outer)
-Workload at N=1 is BASELINE config #2 (125M synthetic GPT-2 tree, 1 GPU, fp32); the same tree
-per rank at every N (weak scaling; configs #3/#4 as N grows). value = N * 4 * params / t_step.
-Rank 0 prints ONE JSON line.
+The headline runs this two-kernel pipeline at every N (BASELINE config #2 at N=1: the
+delta+pack kernels, no RCCL); the one-pass single-replica kernel (dl_delta_sgd, OuterSync's
+default at one replica) is reported beside it. Same tree per rank at every N (weak scaling):
+value = N * 4 * params / t_step. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import platform
 import subprocess
 import sys
 import time
+from datetime import timedelta
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "diloco-swarm_amd"))
@@ -38,21 +41,19 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0       # per link per direction; busBW peak (n-1)*153
 
 
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def load_pmc(tree):
     """Per-launch HBM bytes from the committed rocprofv3 counter passes of the same kernels
     (tools/gpu_pmc.sh -> profiles/rNN_pmc_<tree>.json, FETCH_SIZE x2 gfx950 correction)."""
-    import glob
-
     files = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_pmc_{tree}.json")))
     if not files:
         return {}
     with open(files[-1]) as f:
         d = json.load(f)
     return {k: v["hbm_bytes"] for k, v in d.get("kernels", {}).items()}
-
-
-def log(msg):
-    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def setup_dist(n_gpus):
@@ -64,106 +65,132 @@ def setup_dist(n_gpus):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if ws > 1:
-        from datetime import timedelta
-
         # a hung collective becomes an error after 5 minutes instead of the 10-minute default
         dist.init_process_group("nccl", device_id=dev, timeout=timedelta(minutes=5))
     return ws, rank, dev
 
 
-def build(spec, dev, rank, wire, cap):
+def build(spec, dev, rank, wire, cap, fuse=False):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree_device(spec, dev)
     params = [t.view(s) for t, s in zip(theta0, shapes)]
     eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=wire,
-                    bucket_cap_elems=cap)
+                    bucket_cap_elems=cap, fuse_single=fuse)
     # inner = θ_0 + this rank's noise (stands in for H inner steps)
     synth.inner_tree_device([p.view(-1) for p in params], 1, rank, out=[p.view(-1) for p in params])
     return eng
 
 
-def timed_launches(fn, reps):
-    """Average ms per launch of `fn` over `reps` back-to-back launches, HIP events on the
-    current stream (the stream every dl_* kernel is launched on)."""
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) / reps
+def _max_over_ranks(x, dev, ws):
+    if ws == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
-def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap):
-    eng = build(spec, dev, rank, wire, cap)
+def _sync(ws):
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def kernel_entry(bytes_per_launch, ms, traffic=None, bound="hbm", peak=HBM_PEAK_GBS):
+    ach = bytes_per_launch / (ms * 1e-3) / 1e9
+    return {"bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
+            "frac": round(ach / peak, 4), "traffic": round(traffic) if traffic else None,
+            "bytes_per_launch": bytes_per_launch, "avg_ms": round(ms, 5)}
+
+
+def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loops=True):
+    """Timed region (K outer steps, nothing else on the stream), then an instrumented pass of
+    K more steps with HIP events between the kernels on the stream they run on (events in the
+    timed region would cost the step ~35 us each), then the same kernels back to back."""
+    eng = build(spec, dev, rank, wire, cap, fuse)
     P = spec.total()
     for _ in range(max(warmup, 1)):  # >= 1: the timed steps run the steady-state SGD mode
         eng.step()
-    torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    _sync(ws)
     t0 = time.perf_counter()
     for _ in range(steps):
         eng.step()
+    _sync(ws)
+    dt = _max_over_ranks(time.perf_counter() - t0, dev, ws)
+    wb = 2 if wire == torch.bfloat16 else 4
+    single = ws == 1
+    # instrumented pass (the kernels in their in-step context)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in ev:
+        e[0].record()
+        if single and fuse:
+            eng.step()
+            e[1].record()
+        elif single:
+            eng.pseudo_gradient()
+            e[1].record()
+            eng.apply()
+            eng.steps_done += 1
+        else:
+            eng.step()
+            e[1].record()
+        e[2].record()
     torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    wbytes = 2 if wire == torch.bfloat16 else 4
-    # per-kernel average durations: the same kernels on the same buffers, back to back
-    reps = max(steps, 10)
-    kern_ms = {
-        "delta_pack": timed_launches(eng.pseudo_gradient, reps),
-        "unpack_sgd": timed_launches(eng.apply, reps),
-    }
-    kern_bytes = {
-        "delta_pack": (4 + 4 + wbytes) * P,             # read θ, inner; write wire
-        "unpack_sgd": (wbytes + 4 + 4 + 4 + 4 + 4) * P,  # read wire, θ, buf; write θ, buf, inner
-    }
+    first = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+    second = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
     pmc = load_pmc(spec.name) if wire == torch.float32 else {}
-    kernels = {}
-    for k, b in kern_bytes.items():
-        ms = kern_ms[k]
-        ach = b / (ms * 1e-3) / 1e9
-        tr = pmc.get(k)
-        kernels[k] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                      "traffic": round(tr) if tr else None,
-                      "bytes_per_launch": b, "avg_ms": round(ms, 5)}
-    res = {
-        "tree": spec.name, "params": P, "tensors": len(spec.params()),
-        "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
-        "ms_per_step": dt / steps * 1e3,
-        "value": ws * 4.0 * P / (dt / steps) / 1e9,
-        "kernels": kernels,
-    }
-    if ws == 1:
-        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
-        res["roofline"] = dict(kernels[dom], kernel=dom)
+    res = {"tree": spec.name, "params": P, "tensors": len(spec.params()),
+           "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
+           "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * P / (dt / steps) / 1e9,
+           "wire": "bf16" if wire == torch.bfloat16 else "f32"}
+    if single and fuse:
+        b = 24 * P  # read θ, inner, buf; write θ, buf, inner
+        res["kernels"] = {"delta_sgd": kernel_entry(b, first, pmc.get("delta_sgd"))}
+    elif single:
+        res["kernels"] = {
+            "delta_pack": kernel_entry((8 + wb) * P, first, pmc.get("delta_pack")),
+            "unpack_sgd": kernel_entry((wb + 20) * P, second, pmc.get("unpack_sgd")),
+        }
     else:
-        # the exchange: every bucket's all-reduce back to back (RCCL over xGMI)
+        res["step_ms_instrumented"] = round(first, 4)
+    # the same kernels back to back (cold inputs: no Infinity-Cache reuse across kernels)
+    reps = max(steps, 10)
+
+    def b2b(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    if b2b_loops:
+        res["kernels_b2b"] = {"delta_pack": kernel_entry((8 + wb) * P, b2b(eng.pseudo_gradient)),
+                              "unpack_sgd": kernel_entry((wb + 20) * P, b2b(eng.apply))}
+    if single:
+        ks = res["kernels"]
+        dom = max(ks, key=lambda k: ks[k]["avg_ms"])
+        res["roofline"] = dict(ks[dom], kernel=dom)
+    else:
         def allreduce_all():
             for b in range(eng.tree.n_buckets):
                 eng.all_reduce(b, async_op=False)
-        if ws > 1:
-            dist.barrier()
-        ar_ms = timed_launches(allreduce_all, max(3, steps // 2))
-        t = torch.tensor([ar_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ar_ms = float(t.item())
-        bus = 2.0 * (ws - 1) / ws * wbytes * eng.tree.total
-        ach = bus / (ar_ms * 1e-3) / 1e9
-        peak = (ws - 1) * XGMI_LINK_GBS
-        res["roofline"] = {"bound": "xgmi", "achieved": round(ach, 1), "peak": peak,
-                           "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None,
-                           "kernel": "rccl all_reduce (all buckets)", "avg_ms": round(ar_ms, 4),
-                           "bus_bytes_per_step": bus}
+
+        reps_ar = max(3, steps // 2)
+        _sync(ws)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps_ar):
+            allreduce_all()
+        e1.record()
+        e1.synchronize()
+        ar_ms = _max_over_ranks(e0.elapsed_time(e1) / reps_ar, dev, ws)
+        bus = 2.0 * (ws - 1) / ws * wb * eng.tree.total
+        res["roofline"] = dict(kernel_entry(bus, ar_ms, bound="xgmi",
+                                            peak=(ws - 1) * XGMI_LINK_GBS),
+                               kernel="rccl all_reduce (all buckets, back to back)",
+                               bus_bytes_per_step=bus)
     eng.close()
     del eng
     torch.cuda.empty_cache()
@@ -171,43 +198,43 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap):
 
 
 def parity_check(dev, ws, rank, wire):
-    """The RCCL + HIP path against a plain torch fp32 statement of the same step (tiny tree,
-    many buckets): averaged deltas normwise <= 1e-6 (north-star tolerance) and every replica
-    bit-identical after the full step."""
+    """The HIP (+ RCCL at N > 1) path against a plain torch fp32 statement of the same step
+    on the tiny tree with 3 buckets. fp32 wire: averaged deltas normwise <= 1e-6 (north-star
+    tolerance). bf16 wire: the codec error vs the exact fp32 average, bound n*2^-8. Both: every
+    replica bit-identical after the full step."""
     spec = get_tree("tiny")
     eng = build(spec, dev, rank, wire, 1 << 20)
     nb = eng.tree.n_buckets
     for b in range(nb):
         eng.pseudo_gradient(b)
-        eng.all_reduce(b, async_op=False) if ws > 1 else None
-    got_sum = [t.float().clone() for t in eng.unpacked(eng.wire)]
-    # torch fp32 reference: θ_0 and every rank's inner regenerated locally (counter-based)
+        if ws > 1:
+            eng.all_reduce(b, async_op=False)
+    got = [t.float().reshape(-1) / ws for t in eng.unpacked(eng.wire)]
     theta0 = synth.outer_tree_device(spec, dev)
     acc = [torch.zeros_like(t) for t in theta0]
-    for r in range(ws):
+    for r in range(ws):  # every rank's inner, regenerated locally (counter-based)
         inner_r = synth.inner_tree_device(theta0, 1, r)
-        d = [t - i for t, i in zip(theta0, inner_r)]
-        if wire == torch.bfloat16:
-            d = [x.to(torch.bfloat16).float() for x in d]
-        acc = [a + x for a, x in zip(acc, d)]
+        acc = [a + (t - i) for a, t, i in zip(acc, theta0, inner_r)]
     worst = 0.0
-    for g, ref in zip(got_sum, acc):
-        g = g.reshape(-1) / ws
-        ref = ref / ws
+    for g, a in zip(got, acc):
+        ref = a / ws
         scale = float(ref.abs().max().clamp_min(1e-30))
         worst = max(worst, float((g - ref).abs().max()) / scale)
     for b in range(nb):
         eng.apply(b)
     eng.steps_done += 1
     torch.cuda.synchronize()
-    ck = torch.stack([eng.theta.view(torch.int32).to(torch.int64).sum(),
-                      -eng.theta.view(torch.int32).to(torch.int64).sum()])
+    bits = eng.theta.view(torch.int32).to(torch.int64).sum()
+    ck = torch.stack([bits, -bits])
     if ws > 1:
         dist.all_reduce(ck, op=dist.ReduceOp.MAX)
     identical = bool(ck[0].item() == -ck[1].item())
-    tol = 1e-6 if wire == torch.float32 else 1e-2
+    # bf16: unit roundoff 2^-8 for the cast, plus one rounding per partial sum of the
+    # collective's bf16 reduction (at most ws - 1 of them)
+    tol = 1e-6 if wire == torch.float32 else ws * 2.0 ** -8
     eng.close()
-    return {"tree": "tiny", "buckets": nb, "avg_delta_normwise_err": worst, "tolerance": tol,
+    return {"tree": "tiny", "buckets": nb, "wire": "f32" if wire == torch.float32 else "bf16",
+            "avg_delta_normwise_err": worst, "tolerance": tol,
             "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
 
 
@@ -259,13 +286,13 @@ def dropin_rate(spec, dev, ws, rank, steps):
     t0 = time.perf_counter()
     for _ in range(steps):
         one(True)
-    dt = (time.perf_counter() - t0) / steps
+    dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
     P = spec.total()
     return {"tree": spec.name, "value": round(ws * 4.0 * P / dt / 1e9, 2), "unit": "GB/s",
             "ms_per_step": round(dt * 1e3, 3),
             "phase_ms": {k: round(v / steps * 1e3, 3) for k, v in phases.items()},
-            "pcie_bytes_per_step": (16 if ws > 1 else 12) * P,
-            "note": "host outer model; D2H of delta, (avg), θ, momentum per step"}
+            "d2h_bytes_per_step": (16 if ws > 1 else 12) * P,
+            "note": "host outer model (reference semantics); D2H of delta, (avg,) θ, momentum"}
 
 
 def cpu_baseline(spec, seconds_budget=12.0):
@@ -273,8 +300,7 @@ def cpu_baseline(spec, seconds_budget=12.0):
     sys.path.insert(0, HERE)
     from oracle.torch_restatement import time_steps
 
-    numels = spec.numels()
-    t, n = time_steps(numels, steps=2, threads=1, budget_s=seconds_budget)
+    t, n = time_steps(spec.numels(), steps=2, threads=1, budget_s=seconds_budget)
     model = ""
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -294,6 +320,19 @@ def cpu_baseline(spec, seconds_budget=12.0):
     }
 
 
+def _guard(fn, *a, **k):
+    try:
+        return fn(*a, **k)
+    except Exception as e:  # reported in the JSON line, never hidden
+        log(f"{fn.__name__} failed: {e!r}")
+        return {"ok": False, "error": repr(e)}
+
+
+def _brief(r):
+    keep = ("value", "ms_per_step", "roofline", "kernels", "buckets", "params", "wire")
+    return {k: r[k] for k in keep if k in r}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -305,6 +344,11 @@ def main():
     ap.add_argument("--extra-tree", default="t1.3b", help="second tree measured beside (or 'none')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the host-outer-model rate")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--only-headline", action="store_true",
+                    help="headline tree only (for rocprofv3 runs of the same kernels)")
+    ap.add_argument("--no-b2b", action="store_true",
+                    help="skip the back-to-back kernel loops (rocprofv3 averages = in-step launches)")
     a = ap.parse_args()
 
     ws, rank, dev = setup_dist(a.gpus)
@@ -313,26 +357,29 @@ def main():
     _lib.load()
     spec = get_tree(a.tree)
     log(f"rank {rank}/{ws} tree {spec.name} ({spec.total()} params) wire {a.wire}")
-    main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap)
-    extra = {}
-    if a.extra_tree != "none" and a.extra_tree != a.tree:
-        es = get_tree(a.extra_tree)
-        r = run_tree(es, dev, ws, rank, max(3, a.steps // 4), 1, wire, cap)
-        extra[es.name] = {k: r[k] for k in ("value", "ms_per_step", "roofline", "buckets", "params")}
-    parity = dropin = None
-    try:
-        parity = parity_check(dev, ws, rank, wire)
-    except Exception as e:  # reported, never hidden
-        parity = {"ok": False, "error": repr(e)}
-    if not a.no_dropin:
-        try:
-            dropin = dropin_rate(spec, dev, ws, rank, 5)
-        except Exception as e:
-            dropin = {"error": repr(e)}
-    cpu = None
-    if rank == 0 and ws == 1 and not a.no_cpu_baseline:
-        log("timing the CPU baseline")
-        cpu = cpu_baseline(spec)
+    main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap,
+                        b2b_loops=not a.no_b2b)
+    extra, parity, dropin, cpu = {}, None, None, None
+    if not a.only_headline:
+        if ws == 1:
+            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, cap, True)
+            extra[f"{spec.name}_fused_single"] = _brief(r) if "value" in r else r
+        if a.extra_tree != "none" and a.extra_tree != a.tree:
+            es = get_tree(a.extra_tree)
+            ks = max(3, a.steps // 4)
+            r = _guard(run_tree, es, dev, ws, rank, ks, 1, wire, cap)
+            extra[es.name] = _brief(r) if "value" in r else r
+            if wire == torch.float32:  # BASELINE config #5: bf16 wire + SGD fused into unpack
+                r = _guard(run_tree, es, dev, ws, rank, ks, 1, torch.bfloat16, cap)
+                extra[f"{es.name}_bf16_wire"] = _brief(r) if "value" in r else r
+        if not a.no_parity:
+            parity = {"f32": _guard(parity_check, dev, ws, rank, torch.float32),
+                      "bf16": _guard(parity_check, dev, ws, rank, torch.bfloat16)}
+        if not a.no_dropin:
+            dropin = _guard(dropin_rate, spec, dev, ws, rank, 5)
+        if rank == 0 and ws == 1 and not a.no_cpu_baseline:
+            log("timing the CPU baseline")
+            cpu = cpu_baseline(spec)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -357,7 +404,8 @@ def main():
             },
             "roofline": main_res["roofline"],
             "cpu_baseline": cpu,
-            "kernels": main_res["kernels"],
+            "kernels": main_res.get("kernels"),
+            "kernels_b2b": main_res.get("kernels_b2b"),
             "parity": parity,
             "dropin_pcie": dropin,
             "extra": extra or None,

@@ -65,9 +65,10 @@ struct dl_tree_s {
   std::vector<int64_t> numel, seg_off, bounds;
   std::vector<int32_t> bkt_chunk;  // first chunk of each bucket, + sentinel
   std::vector<dl::Chunk> chunks;
+  std::vector<int64_t> chunk_loff;  // host only: offset of each chunk inside its tensor
   dl::Chunk* d_chunks = nullptr;
-  void** d_ptab = nullptr;
-  uint64_t* h_stage = nullptr;  // pinned staging for pointer-table uploads
+  void** d_caddr = nullptr;     // [DL_MAX_SLOTS][nchunk] resolved chunk addresses
+  uint64_t* h_stage = nullptr;  // pinned staging for address-table uploads (nchunk entries)
   std::vector<uint8_t> bound;   // slot bound?
   std::vector<uint8_t> slot_aligned;
   int32_t grid = 0;                 // 0 = one workgroup per chunk
@@ -117,11 +118,11 @@ DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl
       for (int64_t off = 0; off < t->numel[s]; off += DL_CHUNK_ELEMS) {
         dl::Chunk c{};
         c.poff = t->seg_off[s] + off;
-        c.loff = off;
         c.seg = int32_t(s);
         const int64_t rem = t->numel[s] - off;
         c.len = int32_t(rem < DL_CHUNK_ELEMS ? rem : DL_CHUNK_ELEMS);
         t->chunks.push_back(c);
+        t->chunk_loff.push_back(off);
       }
     }
     if (t->chunks.size() > size_t(INT32_MAX)) {
@@ -134,17 +135,18 @@ DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl
   t->slot_aligned.assign(DL_MAX_SLOTS, 1);
 
   hipError_t e = hipGetDevice(&t->device);
-  const size_t cbytes = (t->chunks.empty() ? 1 : t->chunks.size()) * sizeof(dl::Chunk);
-  const size_t pbytes = size_t(DL_MAX_SLOTS) * (t->nseg > 0 ? t->nseg : 1) * sizeof(void*);
+  const size_t nch = t->chunks.empty() ? 1 : t->chunks.size();
+  const size_t cbytes = nch * sizeof(dl::Chunk);
+  const size_t abytes = size_t(DL_MAX_SLOTS) * nch * sizeof(void*);
   if (e == hipSuccess) e = hipMalloc(&t->d_chunks, cbytes);
-  if (e == hipSuccess) e = hipMalloc(&t->d_ptab, pbytes);
-  if (e == hipSuccess) e = hipMemset(t->d_ptab, 0, pbytes);
+  if (e == hipSuccess) e = hipMalloc(&t->d_caddr, abytes);
+  if (e == hipSuccess) e = hipMemset(t->d_caddr, 0, abytes);
   if (e == hipSuccess && !t->chunks.empty())
     e = hipMemcpy(t->d_chunks, t->chunks.data(), t->chunks.size() * sizeof(dl::Chunk),
                   hipMemcpyHostToDevice);
   if (e == hipSuccess)
-    e = hipHostMalloc(reinterpret_cast<void**>(&t->h_stage),
-                      (t->nseg > 0 ? t->nseg : 1) * sizeof(uint64_t), hipHostMallocDefault);
+    e = hipHostMalloc(reinterpret_cast<void**>(&t->h_stage), nch * sizeof(uint64_t),
+                      hipHostMallocDefault);
   if (e != hipSuccess) {
     int rc2 = hip_fail(e, "dl_tree_create");
     dl_tree_destroy(t);
@@ -157,7 +159,7 @@ DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl
 DL_API int dl_tree_destroy(dl_tree_t t) {
   if (!t) return DL_OK;
   if (t->d_chunks) (void)hipFree(t->d_chunks);
-  if (t->d_ptab) (void)hipFree(t->d_ptab);
+  if (t->d_caddr) (void)hipFree(t->d_caddr);
   if (t->h_stage) (void)hipHostFree(t->h_stage);
   delete t;
   return DL_OK;
@@ -213,7 +215,8 @@ DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t
       return fail(DL_E_ARG, "dl_tree_bind: null address for tensor %d", i);
     if (ptrs[i] & 3u) return fail(DL_E_ALIGN, "dl_tree_bind: tensor %d not 4-B aligned", i);
   }
-  if (n == 0) {
+  const size_t nch = t->chunks.size();
+  if (nch == 0) {
     t->bound[slot] = 1;
     return DL_OK;
   }
@@ -221,8 +224,9 @@ DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t
   // The previous table of this slot may still be read by queued kernels on `s`: the copy is
   // stream-ordered behind them; the staging buffer is reused only after it has landed.
   DL_HIP(hipStreamSynchronize(s), "dl_tree_bind(sync before stage)");
-  std::memcpy(t->h_stage, ptrs, size_t(n) * sizeof(uint64_t));
-  DL_HIP(hipMemcpyAsync(t->d_ptab + size_t(slot) * t->nseg, t->h_stage, size_t(n) * sizeof(void*),
+  for (size_t c = 0; c < nch; ++c)
+    t->h_stage[c] = ptrs[t->chunks[c].seg] + uint64_t(t->chunk_loff[c]) * sizeof(float);
+  DL_HIP(hipMemcpyAsync(t->d_caddr + size_t(slot) * nch, t->h_stage, nch * sizeof(void*),
                         hipMemcpyHostToDevice, s),
          "dl_tree_bind(upload)");
   DL_HIP(hipStreamSynchronize(s), "dl_tree_bind(sync after upload)");
@@ -253,8 +257,8 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
     return fail(DL_E_ARG, "%s: bucket %d of %d", who, b, nb);
   }
   L->chunks = t->d_chunks;
-  L->ptab = t->d_ptab;
-  L->nseg = t->nseg;
+  L->caddr = t->d_caddr;
+  L->nchunk = int32_t(t->chunks.size());
   L->grid = t->grid;
   L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
   L->stream = static_cast<hipStream_t>(s);
@@ -335,6 +339,21 @@ DL_API int dl_unpack_sgd(dl_tree_t t, int32_t b, const void* wire, int32_t wire_
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_unpack_sgd");
 }
 
+DL_API int dl_delta_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer, float* mom,
+                        float lr, float momentum, int32_t nesterov, int32_t first_step,
+                        dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_sgd", kAutoUnpackSgd));
+  DL_TRY(check_slot(t, inner_slot, "dl_delta_sgd"));
+  DL_TRY(check_packed(outer, "dl_delta_sgd", "outer"));
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_delta_sgd", "momentum"));
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_delta_sgd: Nesterov momentum requires a momentum");
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_delta_sgd(L, inner_slot, outer, mom, a);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_sgd");
+}
+
 DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int32_t dtype,
                      dl_stream_t s) {
   dl::Launch L;
@@ -375,18 +394,6 @@ DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_i
   hipError_t e = dl::launch_fill_synth(dst, n, seed, stream_id, base, scale, add,
                                        static_cast<hipStream_t>(s));
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_fill_synth");
-}
-
-DL_API int dl_host_register(void* ptr, int64_t bytes) {
-  if (!ptr || bytes <= 0) return fail(DL_E_ARG, "dl_host_register: bad range");
-  DL_HIP(hipHostRegister(ptr, size_t(bytes), hipHostRegisterDefault), "dl_host_register");
-  return DL_OK;
-}
-
-DL_API int dl_host_unregister(void* ptr) {
-  if (!ptr) return fail(DL_E_ARG, "dl_host_unregister: null");
-  DL_HIP(hipHostUnregister(ptr), "dl_host_unregister");
-  return DL_OK;
 }
 
 }  // extern "C"

@@ -11,16 +11,16 @@ constexpr int kThreads = 256;                          // 4 waves of 64 lanes
 constexpr int kUnroll = DL_CHUNK_ELEMS / (kThreads * 4);  // float4 per lane per chunk (=4)
 static_assert(kUnroll * kThreads * 4 == DL_CHUNK_ELEMS, "chunk must be a whole number of sweeps");
 
-// One work unit: up to DL_CHUNK_ELEMS consecutive elements of one segment. 32 B so a
-// workgroup fetches it with one scalar load.
+// One work unit: up to DL_CHUNK_ELEMS consecutive elements of one segment; 16 B, fetched by
+// a workgroup with one scalar load. The address of the chunk's first element inside each
+// bound per-tensor slot is pre-resolved at bind time (Launch::caddr), so a workgroup's two
+// descriptor loads are independent instead of a chunk -> tensor -> pointer chain.
 struct Chunk {
   int64_t poff;  // offset in the packed space
-  int64_t loff;  // offset inside the segment's own tensor
-  int32_t seg;   // segment (tensor) index in parameters() order
   int32_t len;   // elements, 1..DL_CHUNK_ELEMS
-  int64_t pad_;
+  int32_t seg;   // segment (tensor) index in parameters() order
 };
-static_assert(sizeof(Chunk) == 32, "Chunk layout");
+static_assert(sizeof(Chunk) == 16, "Chunk layout");
 
 inline bool aligned16_host(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -34,8 +34,8 @@ struct SgdArgs {
 struct Launch {
   const Chunk* chunks;  // device chunk table
   int32_t c0, c1;       // chunk range
-  void* const* ptab;    // device pointer table [DL_MAX_SLOTS][nseg]
-  int32_t nseg;
+  void* const* caddr;   // device table [DL_MAX_SLOTS][nchunk]: per-slot address of each chunk
+  int32_t nchunk;
   int32_t grid;   // 0 = one workgroup per chunk
   int32_t flags;  // DL_TUNE_*
   hipStream_t stream;
@@ -47,6 +47,7 @@ hipError_t launch_unpack_avg(const Launch& L, const void* wire, int wire_dtype, 
                              int dst_slot, float* dst_packed);
 hipError_t launch_unpack_sgd(const Launch& L, const void* wire, int wire_dtype, int divisor,
                              float* outer, float* mom, SgdArgs a, int inner_slot);
+hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float* mom, SgdArgs a);
 hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype);
 hipError_t launch_scatter(const Launch& L, const float* packed, int dst_slot);
 hipError_t launch_serialize(const void* src, int src_dtype, int64_t numel, float m0, float m1,

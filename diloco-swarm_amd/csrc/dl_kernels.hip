@@ -122,19 +122,19 @@ __device__ __forceinline__ float4 div4(float4 a, float d) {
 }
 
 template <typename T>
-__device__ __forceinline__ T* slot_ptr(void* const* ptab, int nseg, int slot, const Chunk& ck) {
-  return static_cast<T*>(ptab[slot * nseg + ck.seg]) + ck.loff;
+__device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot, int c) {
+  return static_cast<T*>(caddr[slot * nchunk + c]);
 }
 
 // ---- the walker ----------------------------------------------------------------------------
 // Body::operator() is instantiated per (NTL, NTS) policy: non-temporal loads / stores.
 template <class Body, bool NTL, bool NTS>
 __global__ void __launch_bounds__(kThreads)
-    k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ ptab,
-           int32_t nseg, Body body) {
+    k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ caddr,
+           int32_t nchunk, Body body) {
   for (int32_t c = c0 + int32_t(blockIdx.x); c < c1; c += int32_t(gridDim.x)) {
     const Chunk ck = chunks[c];
-    body.template run<NTL, NTS>(ck, ptab, nseg, int(threadIdx.x));
+    body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x));
   }
 }
 
@@ -145,8 +145,8 @@ struct DeltaPack {
   const float* outer;
   W* wire;
   template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
-    const float* in = slot_ptr<const float>(ptab, nseg, inner_slot, ck);
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    const float* in = slot_ptr<const float>(caddr, nchunk, inner_slot, c);
     const float* th = outer + ck.poff;
     W* w = wire + ck.poff;
     if (aligned16(in)) {
@@ -181,8 +181,8 @@ struct UnpackAvg {
   float* dst_packed;
   float d;
   template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
-    float* dst = dst_slot >= 0 ? slot_ptr<float>(ptab, nseg, dst_slot, ck) : dst_packed + ck.poff;
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    float* dst = dst_slot >= 0 ? slot_ptr<float>(caddr, nchunk, dst_slot, c) : dst_packed + ck.poff;
     const W* w = wire + ck.poff;
     if (aligned16(dst)) {
       const int nv = ck.len >> 2;
@@ -232,8 +232,8 @@ struct UnpackSgd {
   SgdArgs a;
   int inner_slot;
   template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
-    float* in = inner_slot >= 0 ? slot_ptr<float>(ptab, nseg, inner_slot, ck) : nullptr;
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    float* in = inner_slot >= 0 ? slot_ptr<float>(caddr, nchunk, inner_slot, c) : nullptr;
     const W* w = wire + ck.poff;
     float* th = outer + ck.poff;
     float* mb = mom + ck.poff;
@@ -287,14 +287,76 @@ struct UnpackSgd {
   }
 };
 
+// a2+a4+a5 at ONE peer (src/comm.py:118-119: no all-reduce, no division): the delta never
+// leaves registers. g = θ - inner; SGD; θ and inner <- θ'. 24 B/param (20 first step)
+// instead of 12 + 24 for delta_pack + unpack_sgd; results are bit-identical to that pair.
+template <int MODE>
+struct DeltaSgd {
+  float* outer;
+  float* mom;
+  SgdArgs a;
+  int inner_slot;
+  template <bool NTL, bool NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
+    float* th = outer + ck.poff;
+    float* mb = mom + ck.poff;
+    if (aligned16(in)) {
+      const int nv = ck.len >> 2;
+      float4 x[kUnroll], t[kUnroll], m[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int v = u * kThreads + tid;
+        if (v < nv) {
+          t[u] = ldf4<NTL>(th, v);
+          x[u] = ldf4<NTL>(in, v);
+          if (MODE == 2) m[u] = ldf4<NTL>(mb, v);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int v = u * kThreads + tid;
+        if (v < nv) {
+          const float4 g = sub4(t[u], x[u]);
+          sgd1<MODE>(g.x, m[u].x, t[u].x, a);
+          sgd1<MODE>(g.y, m[u].y, t[u].y, a);
+          sgd1<MODE>(g.z, m[u].z, t[u].z, a);
+          sgd1<MODE>(g.w, m[u].w, t[u].w, a);
+          stf4<NTS>(th, v, t[u]);
+          if (MODE != 0) stf4<NTS>(mb, v, m[u]);
+          stf4<NTS>(in, v, t[u]);
+        }
+      }
+      const int i = (nv << 2) + tid;
+      if (i < ck.len) {
+        const float g = th[i] - in[i];
+        float b = (MODE == 2) ? mb[i] : 0.f, t1 = th[i];
+        sgd1<MODE>(g, b, t1, a);
+        th[i] = t1;
+        if (MODE != 0) mb[i] = b;
+        in[i] = t1;
+      }
+    } else {
+      for (int i = tid; i < ck.len; i += kThreads) {
+        const float g = th[i] - in[i];
+        float b = (MODE == 2) ? mb[i] : 0.f, t1 = th[i];
+        sgd1<MODE>(g, b, t1, a);
+        th[i] = t1;
+        if (MODE != 0) mb[i] = b;
+        in[i] = t1;
+      }
+    }
+  }
+};
+
 // per-tensor fp32 -> packed W
 template <typename W>
 struct Gather {
   int src_slot;
   W* packed;
   template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
-    const float* src = slot_ptr<const float>(ptab, nseg, src_slot, ck);
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    const float* src = slot_ptr<const float>(caddr, nchunk, src_slot, c);
     W* p = packed + ck.poff;
     if (aligned16(src)) {
       const int nv = ck.len >> 2;
@@ -322,8 +384,8 @@ struct Scatter {
   const float* packed;
   int dst_slot;
   template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, void* const* ptab, int nseg, int tid) const {
-    float* dst = slot_ptr<float>(ptab, nseg, dst_slot, ck);
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    float* dst = slot_ptr<float>(caddr, nchunk, dst_slot, c);
     const float* p = packed + ck.poff;
     if (aligned16(dst)) {
       const int nv = ck.len >> 2;
@@ -349,7 +411,7 @@ struct Scatter {
 template <class Body, bool NTL, bool NTS>
 hipError_t run_policy(const Launch& L, const Body& body, int32_t grid) {
   hipLaunchKernelGGL((k_walk<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream, L.chunks,
-                     L.c0, L.c1, L.ptab, L.nseg, body);
+                     L.c0, L.c1, L.caddr, L.nchunk, body);
   return hipGetLastError();
 }
 
@@ -476,6 +538,12 @@ hipError_t launch_unpack_sgd(const Launch& L, const void* wire, int wire_dtype, 
   if (wire_dtype == DL_BF16)
     return unpack_sgd_t(L, static_cast<const bf16_t*>(wire), divisor, outer, mom, a, inner_slot);
   return unpack_sgd_t(L, static_cast<const float*>(wire), divisor, outer, mom, a, inner_slot);
+}
+
+hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float* mom, SgdArgs a) {
+  if (a.momentum == 0.f) return run(L, DeltaSgd<0>{outer, mom, a, inner_slot});
+  if (a.first) return run(L, DeltaSgd<1>{outer, mom, a, inner_slot});
+  return run(L, DeltaSgd<2>{outer, mom, a, inner_slot});
 }
 
 hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype) {

@@ -46,12 +46,11 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _i32, _vp],
     ),
+    "dl_delta_sgd": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _vp]),
     "dl_gather": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp]),
     "dl_scatter": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp]),
     "dl_serialize": (ctypes.c_int, [_vp, _i32, _i64, _f32, _f32, _vp, _vp]),
     "dl_fill_synth": (ctypes.c_int, [_vp, _i64, _u64, _u64, _f32, _f32, _vp, _vp]),
-    "dl_host_register": (ctypes.c_int, [_vp, _i64]),
-    "dl_host_unregister": (ctypes.c_int, [_vp]),
     "dl_last_error": (ctypes.c_char_p, []),
     "dl_abi_version": (ctypes.c_int, []),
 }

@@ -106,43 +106,14 @@ class RecvThread:
 DP_BACKEND = os.environ.get("DILOCO_DP_BACKEND", "nccl")
 
 
-class TrainingComm:
-    def __init__(self, world, shape: Tuple[int, ...], logger):
-        self.world, self.shape, self.logger = world, shape, logger
-        kw = {"tag": 0, "serialize": True, "requires_grad": True, "logger": logger}
-        self.forward_send_thread = SendThread(shape, group=world.next_stage_group,
-                                              start=world.has_next_stage, **kw)
-        self.backward_recv_thread = RecvThread(shape, group=world.next_stage_group,
-                                               start=world.has_next_stage, **kw)
-        self.backward_send_thread = SendThread(shape, group=world.prev_stage_group,
-                                               start=world.has_prev_stage, **kw)
-        self.forward_recv_thread = RecvThread(shape, group=world.prev_stage_group,
-                                              start=world.has_prev_stage, **kw)
+class DPSync:
+    """The DP average of one stage's gradients (src/comm.py:117-123) on the GPU."""
+
+    def __init__(self, world):
+        self.world = world
         self._rccl_group = None
         self._grad_syncs: Dict[int, GradSync] = {}
 
-    # ---- pipeline p2p (unchanged protocol) ----------------------------------------------
-    def send_forward(self, tensor: torch.Tensor, metadata: Metadata) -> None:
-        if not self.world.has_next_stage:
-            return
-        dst = random.choice(self.world.stage2ranks[self.world.stage + 1])
-        self.forward_send_thread.send(dst=dst, tensor=tensor, metadata=metadata)
-
-    def send_backward(self, dst: int, tensor: torch.Tensor, metadata: Metadata) -> None:
-        if not self.world.has_prev_stage:
-            return
-        self.backward_send_thread.send(dst=dst, tensor=tensor, metadata=metadata)
-
-    def recv_forward(self):
-        return self.forward_recv_thread.receive()
-
-    def recv_backward(self):
-        return self.backward_recv_thread.receive()
-
-    def load_forward(self, metadata: Metadata) -> None:
-        self.forward_recv_thread.load(tensor=None, metadata=metadata)
-
-    # ---- the DP sync (outer-step hot path) ----------------------------------------------
     @property
     def num_peers(self) -> int:
         return len(self.world.stage2ranks[self.world.stage])
@@ -181,6 +152,59 @@ class TrainingComm:
             gs = GradSync(params, self.dp_group(params[0].device), num_peers)
             self._grad_syncs[id(model)] = gs
         gs.sync()
+
+
+_DP: Dict[int, DPSync] = {}
+
+
+def dp_sync_gradients(world, model: nn.Module) -> None:
+    """Module-level entry for a reference TrainingComm whose sync_gradients delegates here
+    (INTEGRATION.md); one DPSync (and RCCL group) per World object."""
+    d = _DP.get(id(world))
+    if d is None or d.world is not world:
+        d = _DP[id(world)] = DPSync(world)
+    d.sync_gradients(model)
+
+
+class TrainingComm:
+    def __init__(self, world, shape: Tuple[int, ...], logger):
+        self.world, self.shape, self.logger = world, shape, logger
+        kw = {"tag": 0, "serialize": True, "requires_grad": True, "logger": logger}
+        self.forward_send_thread = SendThread(shape, group=world.next_stage_group,
+                                              start=world.has_next_stage, **kw)
+        self.backward_recv_thread = RecvThread(shape, group=world.next_stage_group,
+                                               start=world.has_next_stage, **kw)
+        self.backward_send_thread = SendThread(shape, group=world.prev_stage_group,
+                                               start=world.has_prev_stage, **kw)
+        self.forward_recv_thread = RecvThread(shape, group=world.prev_stage_group,
+                                              start=world.has_prev_stage, **kw)
+        self.dp = DPSync(world)
+
+    # ---- pipeline p2p (unchanged protocol) ----------------------------------------------
+    def send_forward(self, tensor: torch.Tensor, metadata: Metadata) -> None:
+        if not self.world.has_next_stage:
+            return
+        dst = random.choice(self.world.stage2ranks[self.world.stage + 1])
+        self.forward_send_thread.send(dst=dst, tensor=tensor, metadata=metadata)
+
+    def send_backward(self, dst: int, tensor: torch.Tensor, metadata: Metadata) -> None:
+        if not self.world.has_prev_stage:
+            return
+        self.backward_send_thread.send(dst=dst, tensor=tensor, metadata=metadata)
+
+    def recv_forward(self):
+        return self.forward_recv_thread.receive()
+
+    def recv_backward(self):
+        return self.backward_recv_thread.receive()
+
+    def load_forward(self, metadata: Metadata) -> None:
+        self.forward_recv_thread.load(tensor=None, metadata=metadata)
+
+    # ---- the DP sync (outer-step hot path) ----------------------------------------------
+    def sync_gradients(self, model: nn.Module) -> None:
+        """src/comm.py:117-123 on RCCL + HIP (see DPSync)."""
+        self.dp.sync_gradients(model)
 
     # ---- metrics aggregation (src/comm.py:125-149) ---------------------------------------
     def sync_outputs(self, outputs):

@@ -61,6 +61,11 @@ class HipKernels:
                   int(divisor), theta.data_ptr(), _ptr(mom), float(lr), float(momentum),
                   int(nesterov), int(first), int(inner_slot), _s(theta))
 
+    def delta_sgd(self, tree, bucket, inner_slot, theta, mom, lr, momentum, nesterov,
+                  first) -> None:
+        _lib.call("dl_delta_sgd", tree.handle, bucket, inner_slot, theta.data_ptr(), _ptr(mom),
+                  float(lr), float(momentum), int(nesterov), int(first), _s(theta))
+
     def unpack_avg(self, tree, bucket, wire, divisor, dst_slot, dst_packed=None) -> None:
         _lib.call("dl_unpack_avg", tree.handle, bucket, wire.data_ptr(), wire_code(wire.dtype),
                   int(divisor), int(dst_slot), _ptr(dst_packed), _s(wire))

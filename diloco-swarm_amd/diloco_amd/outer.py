@@ -8,6 +8,10 @@ One `OuterSync` per DP replica (one process per GPU). It performs, for the whole
     outer_optimizer.step()    (src/train.py:267)      -> dl_unpack_sgd   g = wire/n; Nesterov SGD
     sync_inner_model          (src/utils.py:223-226)  -> (fused in dl_unpack_sgd) inner = θ
 
+With one replica (no all-reduce, src/comm.py:118-119) the default is a single pass,
+dl_delta_sgd: the delta stays in registers (24 instead of 36 B/param); fuse_single=False
+keeps the two-kernel pipeline (BASELINE config #2's delta+pack -> unpack).
+
 Layout in HBM (DESIGN.md "Data layout"): θ_outer, momentum and the wire buffer are packed
 fp32 (wire optionally bf16) arrays in parameters() order with 256-B-aligned segments; the
 inner parameters stay where PyTorch allocated them and are reached through a device pointer
@@ -63,6 +67,7 @@ class OuterSync:
         wire_dtype: torch.dtype = torch.float32,
         bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS,
         kernels=None,
+        fuse_single: bool = True,
     ):
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
                                            for p in params]
@@ -74,6 +79,8 @@ class OuterSync:
         self.device = self.params[0].device
         self.lr, self.momentum, self.nesterov = float(lr), float(momentum), bool(nesterov)
         self.wire_dtype = wire_dtype
+        # one replica: delta + SGD + copy-back in one pass (dl_delta_sgd), no wire round trip
+        self.fuse_single = bool(fuse_single)
         self.group = group
         if world_size is None:
             world_size = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -116,8 +123,12 @@ class OuterSync:
     # ---- the outer step ---------------------------------------------------------------------
     def step(self) -> None:
         """One DiLoCo outer step over the whole tree (src/train.py:261-269)."""
-        if self.world_size == 1:
+        if self.world_size == 1 and self.fuse_single:
             # src/comm.py:118-119: one peer -> no all-reduce and no division
+            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+            self.k.delta_sgd(self.tree, ALL, SLOT_INNER, self.theta, self.mom, self.lr,
+                             self.momentum, self.nesterov, self.steps_done == 0)
+        elif self.world_size == 1:
             self.pseudo_gradient(ALL)
             self.apply(ALL)
         else:

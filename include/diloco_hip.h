@@ -115,6 +115,14 @@ DL_API int dl_unpack_sgd(dl_tree_t tree, int32_t bucket, const void* wire, int32
                          float momentum, int32_t nesterov, int32_t first_step,
                          int32_t inner_slot, dl_stream_t stream);
 
+/* a2+a4+a5 at ONE peer (src/comm.py:118-119 skips the all-reduce and the division):
+ *   g = θ - inner[seg][j]; SGD as dl_unpack_sgd; θ and inner[seg][j] <- new θ
+ * One pass, the delta stays in registers: 24 B/param (20 on the first step) instead of 36
+ * for dl_delta_pack + dl_unpack_sgd; bit-identical results. */
+DL_API int dl_delta_sgd(dl_tree_t tree, int32_t bucket, int32_t inner_slot, float* outer_packed,
+                        float* mom_packed, float lr, float momentum, int32_t nesterov,
+                        int32_t first_step, dl_stream_t stream);
+
 /* Gather per-tensor fp32 (slot) into a packed buffer of dtype `dtype` (fp32 or bf16).
  * Used to pack device gradients (DP sync, src/comm.py:117-123 with device grads, called at
  * src/train.py:251) and to initialise the device θ_outer mirror (src/utils.py:215). */
@@ -138,10 +146,6 @@ DL_API int dl_serialize(const void* src, int32_t src_dtype, int64_t numel, float
  * all fp32 ops correctly rounded: bit-identical to diloco_amd.synth (numpy). */
 DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id, float base,
                          float scale, const float* add, dl_stream_t stream);
-
-/* ---- host memory for the host-resident outer copy (src/utils.py:216) ------------------ */
-DL_API int dl_host_register(void* ptr, int64_t bytes);
-DL_API int dl_host_unregister(void* ptr);
 
 DL_API const char* dl_last_error(void);
 DL_API int dl_abi_version(void);

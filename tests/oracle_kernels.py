@@ -78,6 +78,18 @@ class OracleKernels:
             if inner_slot >= 0:
                 _np(tree.slots[inner_slot][i])[:] = th
 
+    def delta_sgd(self, tree, bucket, inner_slot, theta, mom, lr, momentum, nesterov, first):
+        for i in tree.segs(bucket):
+            th = self._seg(tree, theta, i).copy()
+            inner = _np(tree.slots[inner_slot][i])
+            g = oracle.delta(th, inner.copy())
+            b = self._seg(tree, mom, i).copy() if mom is not None else None
+            oracle.sgd(th, b, g, lr, momentum, nesterov, first)
+            self._seg(tree, theta, i)[:] = th
+            if mom is not None:
+                self._seg(tree, mom, i)[:] = b
+            inner[:] = th
+
     def unpack_avg(self, tree, bucket, wire, divisor, dst_slot, dst_packed=None):
         for i in tree.segs(bucket):
             g = self._seg(tree, wire, i).copy()

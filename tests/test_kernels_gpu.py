@@ -247,3 +247,50 @@ def test_kernel_argument_errors_are_raised():
         _lib.call("dl_unpack_avg", tree.handle, -1, buf.data_ptr(), _lib.DL_F32, 0, SLOT_INNER,
                   None, s)
     tree.close()
+
+
+@pytest.mark.parametrize("tree", ["micro", "tiny"])
+def test_fused_single_peer_step_matches_reference(tree):
+    """dl_delta_sgd (one replica: delta + SGD + copy-back in one pass) vs the reference."""
+    spec = get_tree(tree)
+    theta0 = synth.outer_tree_device(spec, DEV)
+    shapes = [s for _, s in spec.params()]
+    params = [t.clone().view(s) for t, s in zip(theta0, shapes)]
+    e = OuterSync(params, world_size=1, fuse_single=True)
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        e.step()
+        torch.cuda.synchronize()
+        got_t = _host(e.unpacked(e.theta))
+        got_m = _host(e.unpacked(e.mom))
+        assert np.concatenate(_host(params)).tobytes() == np.concatenate(got_t).tobytes()
+        if tree == "micro":
+            g = load_npz("micro_n1.npz")
+            assert np.concatenate(got_t).tobytes() == g[f"theta_s{s}"].tobytes()
+            assert np.concatenate(got_m).tobytes() == g[f"buf_s{s}"].tobytes()
+        else:
+            ref = load_json("tiny_digests.json")["1"]["rank0"]
+            for t, (a, d) in enumerate(zip(got_t, ref[f"theta_s{s}"])):
+                assert _sha(a) == d["sha256"], t
+
+
+@pytest.mark.parametrize("momentum,nesterov", [(0.9, True), (0.9, False), (0.0, False)])
+def test_fused_single_peer_ragged_vs_two_kernel_path(momentum, nesterov):
+    g0 = torch.Generator().manual_seed(5)
+    host = [torch.randn(n, generator=g0) for n in RAGGED]
+    pa = [h.to(DEV) for h in host]
+    pb = [h.to(DEV) for h in host]
+    ea = OuterSync(pa, momentum=momentum, nesterov=nesterov, world_size=1, fuse_single=True)
+    eb = OuterSync(pb, momentum=momentum, nesterov=nesterov, world_size=1, fuse_single=False)
+    for _ in range(3):
+        noise = [torch.randn(n, generator=g0).to(DEV) * 1e-3 for n in RAGGED]
+        for p, q, z in zip(pa, pb, noise):
+            p.add_(z)
+            q.add_(z)
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        for p, q in zip(pa, pb):
+            assert p.cpu().numpy().tobytes() == q.cpu().numpy().tobytes()
+        assert ea.theta.cpu().numpy().tobytes() == eb.theta.cpu().numpy().tobytes()

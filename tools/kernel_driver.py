@@ -27,6 +27,10 @@ def main():
         eng.pseudo_gradient()
     for _ in range(reps):
         eng.apply()
+    fused = OuterSync(params, world_size=1, fuse_single=True)
+    fused.step()
+    for _ in range(reps):
+        fused.step()
     torch.cuda.synchronize()
     print(f"kernel_driver: {tree} x{reps} done")
 

@@ -16,11 +16,13 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("DeltaPack", "UnpackSgd", "UnpackAvg", "Gather", "Scatter", "k_fill_synth"):
+    names = {"DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd", "UnpackAvg": "unpack_avg",
+             "DeltaSgd": "delta_sgd", "Gather": "gather", "Scatter": "scatter",
+             "k_fill_synth": "fill_synth"}
+    for k, v in names.items():
         if k in name:
-            return {"DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd", "UnpackAvg": "unpack_avg",
-                    "Gather": "gather", "Scatter": "scatter", "k_fill_synth": "fill_synth"}[k] + (
-                        "_first" if "UnpackSgd" in name and ", 1>" in name else "")
+            first = (k == "UnpackSgd" and ", 1>" in name) or (k == "DeltaSgd" and "DeltaSgd<1>" in name)
+            return v + ("_first" if first else "")
     return None
 
 
