@@ -295,6 +295,31 @@ def dropin_rate(spec, dev, ws, rank, steps):
             "note": "host outer model (reference semantics); D2H of delta, (avg,) θ, momentum"}
 
 
+def gradsync_rate(spec, dev, ws, rank, steps):
+    """Per-step DP gradient average of device grads (src/train.py:249-251,
+    src/comm.py:117-123): dl_gather -> RCCL all_reduce -> dl_unpack_avg, pipelined buckets."""
+    from diloco_amd.gradsync import GradSync
+
+    shapes = [s for _, s in spec.params()]
+    params = [torch.nn.Parameter(t.view(s))
+              for t, s in zip(synth.outer_tree_device(spec, dev), shapes)]
+    for i, p in enumerate(params):
+        p.grad = torch.empty_like(p)
+        synth.fill_device(p.grad.view(-1), synth.noise_seed(9, rank), i, 0.0, 1e-3)
+    gs = GradSync(params, None, ws)
+    gs.sync()
+    _sync(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gs.sync()
+    _sync(ws)
+    dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
+    P = spec.total()
+    gs.close()
+    return {"tree": spec.name, "value": round(ws * 4.0 * P / dt / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(dt * 1e3, 4), "buckets": gs.tree.n_buckets}
+
+
 def cpu_baseline(spec, seconds_budget=12.0):
     """The reference's per-tensor CPU sequence (oracle/torch_restatement.py), 1 thread."""
     sys.path.insert(0, HERE)
@@ -372,6 +397,9 @@ def main():
             if wire == torch.float32:  # BASELINE config #5: bf16 wire + SGD fused into unpack
                 r = _guard(run_tree, es, dev, ws, rank, ks, 1, torch.bfloat16, cap)
                 extra[f"{es.name}_bf16_wire"] = _brief(r) if "value" in r else r
+        if ws > 1:
+            extra[f"{spec.name}_dp_grad_sync"] = _guard(gradsync_rate, spec, dev, ws, rank,
+                                                        max(3, a.steps // 2))
         if not a.no_parity:
             parity = {"f32": _guard(parity_check, dev, ws, rank, torch.float32),
                       "bf16": _guard(parity_check, dev, ws, rank, torch.bfloat16)}

@@ -121,19 +121,24 @@ class OuterSync:
                           SLOT_INNER if write_inner else -1)
 
     # ---- the outer step ---------------------------------------------------------------------
-    def step(self) -> None:
-        """One DiLoCo outer step over the whole tree (src/train.py:261-269)."""
-        if self.world_size == 1 and self.fuse_single:
+    def step(self, pipeline: Optional[bool] = None) -> None:
+        """One DiLoCo outer step over the whole tree (src/train.py:261-269).
+
+        pipeline=True runs the bucketed collective path even for a single replica (an
+        identity all-reduce): it validates the transport on a one-GPU machine."""
+        if pipeline is None:
+            pipeline = self.world_size > 1
+        if pipeline:
+            pipelined_buckets(self.tree.n_buckets, self.pseudo_gradient,
+                              lambda b: self.all_reduce(b, async_op=True), self.apply)
+        elif self.fuse_single:
             # src/comm.py:118-119: one peer -> no all-reduce and no division
             self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.delta_sgd(self.tree, ALL, SLOT_INNER, self.theta, self.mom, self.lr,
                              self.momentum, self.nesterov, self.steps_done == 0)
-        elif self.world_size == 1:
+        else:
             self.pseudo_gradient(ALL)
             self.apply(ALL)
-        else:
-            pipelined_buckets(self.tree.n_buckets, self.pseudo_gradient,
-                              lambda b: self.all_reduce(b, async_op=True), self.apply)
         self.steps_done += 1
 
     def unpacked(self, packed: torch.Tensor) -> List[torch.Tensor]:

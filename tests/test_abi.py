@@ -88,3 +88,23 @@ def test_missing_library_is_an_import_error(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(ImportError, match="no CPU fallback"):
         _lib.load()
+
+
+def test_planner_fuzz_against_oracle_rule():
+    """Random trees and caps: the C planner == the oracle's C rule == the Python statement."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from oracle import oracle
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.lists(st.integers(0, 300_000), max_size=60), st.integers(-1, 400_000),
+           st.sampled_from([1, 4, 64, 256]))
+    def check(numels, cap, align):
+        seg, bnd = plan_tables(numels, cap, align)
+        oseg, obnd = oracle.plan_tables(numels, cap, align)
+        pseg, pbnd = oracle.plan_tables_py(numels, cap, align)
+        assert seg.tolist() == oseg.tolist() == list(pseg)
+        assert bnd.tolist() == obnd.tolist() == list(pbnd)
+
+    check()

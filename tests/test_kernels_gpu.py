@@ -294,3 +294,32 @@ def test_fused_single_peer_ragged_vs_two_kernel_path(momentum, nesterov):
         for p, q in zip(pa, pb):
             assert p.cpu().numpy().tobytes() == q.cpu().numpy().tobytes()
         assert ea.theta.cpu().numpy().tobytes() == eb.theta.cpu().numpy().tobytes()
+
+
+def test_t13b_full_size_sampled_tensors_vs_oracle_and_fused():
+    """BASELINE configs #4/#5 tree at full size (1.31 B params): the two-kernel path equals the
+    one-pass kernel everywhere (size-independent property), and the largest (wte, 103 M),
+    first-block and last tensors equal the C oracle bit for bit."""
+    spec = get_tree("t1.3b")
+    shapes = [s for _, s in spec.params()]
+    pa = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
+    pb = [t.clone() for t in pa]
+    ea = OuterSync(pa, world_size=1, fuse_single=False)
+    eb = OuterSync(pb, world_size=1, fuse_single=True)
+    for e, ps in ((ea, pa), (eb, pb)):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, 1, 0, out=[p.view(-1) for p in ps])
+        e.step()
+    torch.cuda.synchronize()
+    assert torch.equal(ea.theta, eb.theta) and torch.equal(ea.mom, eb.mom)
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    numels, init = spec.numels(), spec.init_spec()
+    for t in (0, 2, 4, len(numels) - 1):
+        th0 = synth.values(synth.OUTER_SEED, t, numels[t], *init[t])
+        inner = synth.values(synth.noise_seed(1, 0), t, numels[t], 0.0, synth.NOISE_SCALE, add=th0)
+        st = oracle.OuterState([th0])
+        st.step([[inner]])
+        got = ea.unpacked(ea.theta)[t].reshape(-1).cpu().numpy()
+        assert got.tobytes() == st.theta[0].tobytes(), t
+    ea.close()
+    eb.close()

@@ -1,0 +1,125 @@
+"""The RCCL transport on the one-GPU box: a single-rank `nccl` process group.
+
+RCCL refuses two ranks on one device, so multi-peer sums are covered elsewhere (gloo on CPU,
+gloo on one GPU, bench.py's parity self-check at N > 1). Here every collective code path --
+async all_reduce on wire buckets, work.wait() ordering against the HIP kernels on the compute
+stream, bf16 wires, device-gradient packing, the host mirror's device all-reduce -- runs over
+a real RCCL communicator (an identity reduction) and must reproduce the reference bit-exact.
+"""
+import os
+import socket
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO, load_npz
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _flat(ts):
+    return np.concatenate([t.detach().float().cpu().numpy().reshape(-1) for t in ts])
+
+
+def _worker(rank, port, out):
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from datetime import timedelta
+
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                            timeout=timedelta(seconds=120))
+    from diloco_amd import synth
+    from diloco_amd.gradsync import GradSync
+    from diloco_amd.outer import OuterSync
+    from diloco_amd.trees import get_tree
+
+    rec = {}
+    # 1. engine, bucketed pipeline through RCCL, micro tree, many buckets
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+    eng = OuterSync(params, world_size=1, bucket_cap_elems=4096)
+    assert eng.tree.n_buckets > 2
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in eng.unpacked(eng.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        eng.step(pipeline=True)
+        torch.cuda.synchronize()
+        rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
+        rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.mom))
+        rec[f"inner_s{s}"] = _flat(params)
+    # 2. T125 through RCCL (16 buckets) == the fused one-pass kernel, 2 steps
+    spec = get_tree("t125")
+    shapes = [s for _, s in spec.params()]
+    pa = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+    pb = [t.clone() for t in pa]
+    ea = OuterSync(pa, world_size=1, bucket_cap_elems=8 << 20)
+    eb = OuterSync(pb, world_size=1, fuse_single=True)
+    rec["t125_buckets"] = np.array([ea.tree.n_buckets])
+    for s in (1, 2):
+        for e, ps in ((ea, pa), (eb, pb)):
+            th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+            synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in ps])
+        ea.step(pipeline=True)
+        eb.step()
+    torch.cuda.synchronize()
+    rec["t125_equal"] = np.array([bool(torch.equal(ea.theta, eb.theta)) and
+                                  bool(torch.equal(ea.mom, eb.mom)) and
+                                  all(torch.equal(x, y) for x, y in zip(pa, pb))])
+    ea.close()
+    eb.close()
+    del ea, eb, pa, pb
+    # 3. bf16 wire through RCCL == bf16 wire without the collective
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    qa = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+    qb = [t.clone() for t in qa]
+    fa = OuterSync(qa, world_size=1, wire_dtype=torch.bfloat16, bucket_cap_elems=4096)
+    fb = OuterSync(qb, world_size=1, wire_dtype=torch.bfloat16, fuse_single=False)
+    for e, ps in ((fa, qa), (fb, qb)):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, 1, 0, out=[p.view(-1) for p in ps])
+    fa.step(pipeline=True)
+    fb.step()
+    torch.cuda.synchronize()
+    rec["bf16_equal"] = np.array([bool(torch.equal(fa.theta, fb.theta))])
+    # 4. device-gradient DP sync (GradSync) through RCCL: identity average
+    g = torch.Generator().manual_seed(9)
+    gp = [torch.nn.Parameter(torch.zeros(n, device="cuda:0")) for n in (1, 3, 5000, 64, 4097)]
+    for p in gp:
+        p.grad = torch.randn(p.numel(), generator=g).cuda()
+    before = [p.grad.clone() for p in gp]
+    GradSync(gp, None, 1, bucket_cap_elems=4096).sync()
+    torch.cuda.synchronize()
+    rec["gradsync_equal"] = np.array([all(torch.equal(a, p.grad) for a, p in zip(before, gp))])
+    np.savez(os.path.join(out, "rccl.npz"), **rec)
+    dist.destroy_process_group()
+
+
+def test_rccl_single_rank_transport_bit_exact():
+    out = tempfile.mkdtemp(prefix="dl_rccl_")
+    mp.spawn(_worker, args=(_free_port(), out), nprocs=1, join=True)
+    rec = dict(np.load(os.path.join(out, "rccl.npz")))
+    g = load_npz("micro_n1.npz")
+    for s in (1, 2):
+        assert rec[f"theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+        assert rec[f"buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes()
+        assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+    assert rec["t125_buckets"][0] >= 8
+    assert rec["t125_equal"][0]
+    assert rec["bf16_equal"][0]
+    assert rec["gradsync_equal"][0]
