@@ -33,12 +33,24 @@ class GradSync:
         self.numels = [p.numel() for p in self.params]
         self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems)
         self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, device=self.device)
+        # own stream, joined back into the caller's (see OuterSync.stream)
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
 
     def matches(self, params: Sequence[torch.Tensor]) -> bool:
         return len(params) == len(self.params) and all(
             a is b for a, b in zip(params, self.params))
 
     def sync(self) -> None:
+        if self.stream is None:
+            self._sync()
+            return
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self._sync()
+        cur.wait_stream(self.stream)
+
+    def _sync(self) -> None:
         grads = [p.grad for p in self.params]
         for i, g in enumerate(grads):
             if g.dtype != torch.float32 or not g.is_contiguous():

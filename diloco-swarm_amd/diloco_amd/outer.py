@@ -68,6 +68,7 @@ class OuterSync:
         bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS,
         kernels=None,
         fuse_single: bool = True,
+        side_stream: bool = True,
     ):
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
                                            for p in params]
@@ -96,6 +97,12 @@ class OuterSync:
         self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, **z)
         self.k.gather(self.tree, ALL, SLOT_INNER, self.theta)
         self.steps_done = 0
+        # step() runs on its own stream, ordered after the caller's current stream and joined
+        # back into it: work other threads put on the default stream meanwhile (the
+        # reference's p2p send threads copy activations with .to("cpu"), src/comm.py:38)
+        # overlaps the outer step instead of queueing behind it.
+        self.stream = (torch.cuda.Stream(self.device)
+                       if side_stream and self.device.type == "cuda" else None)
 
     # ---- building blocks (each stream-ordered on the current stream) ----------------------
     def pseudo_gradient(self, bucket: int = ALL) -> None:
@@ -126,6 +133,16 @@ class OuterSync:
 
         pipeline=True runs the bucketed collective path even for a single replica (an
         identity all-reduce): it validates the transport on a one-GPU machine."""
+        if self.stream is None:
+            self._step(pipeline)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self._step(pipeline)
+        cur.wait_stream(self.stream)
+
+    def _step(self, pipeline: Optional[bool]) -> None:
         if pipeline is None:
             pipeline = self.world_size > 1
         if pipeline:
