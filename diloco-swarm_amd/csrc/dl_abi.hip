@@ -195,6 +195,20 @@ DL_API int dl_tree_bucket_range(dl_tree_t t, int32_t b, int64_t* begin, int64_t*
   return DL_OK;
 }
 
+DL_API int dl_tree_bucket_chunks(dl_tree_t t, int32_t b, int32_t* c0, int32_t* c1) {
+  if (!t || !c0 || !c1) return fail(DL_E_ARG, "dl_tree_bucket_chunks: null argument");
+  const int32_t nb = int32_t(t->bounds.size()) - 1;
+  if (b == DL_ALL_BUCKETS) {
+    *c0 = 0;
+    *c1 = int32_t(t->chunks.size());
+    return DL_OK;
+  }
+  if (b < 0 || b >= nb) return fail(DL_E_ARG, "dl_tree_bucket_chunks: bucket %d of %d", b, nb);
+  *c0 = t->bkt_chunk[b];
+  *c1 = t->bkt_chunk[b + 1];
+  return DL_OK;
+}
+
 DL_API int dl_tree_tune(dl_tree_t t, int32_t max_blocks, int32_t flags) {
   if (!t || max_blocks < 0) return fail(DL_E_ARG, "dl_tree_tune: bad argument");
   if (flags != DL_TUNE_AUTO && (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES)))
@@ -352,6 +366,45 @@ DL_API int dl_delta_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer
   dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
   hipError_t e = dl::launch_delta_sgd(L, inner_slot, outer, mom, a);
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_sgd");
+}
+
+DL_API int dl_delta_q8(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,
+                       void* slots, dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_q8", kAutoDelta));
+  DL_TRY(check_slot(t, inner_slot, "dl_delta_q8"));
+  DL_TRY(check_packed(outer, "dl_delta_q8", "outer"));
+  DL_TRY(check_packed(slots, "dl_delta_q8", "slots"));
+  hipError_t e = dl::launch_delta_q8(L, inner_slot, outer, static_cast<uint8_t*>(slots));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_q8");
+}
+
+DL_API int dl_q8_reduce(const void* recv, int32_t n, int32_t m, int32_t divisor, void* out,
+                        dl_stream_t s) {
+  if (n < 1 || m < 0 || divisor < 1) return fail(DL_E_ARG, "dl_q8_reduce: n %d m %d div %d", n, m, divisor);
+  DL_TRY(check_packed(recv, "dl_q8_reduce", "recv"));
+  DL_TRY(check_packed(out, "dl_q8_reduce", "out"));
+  if (recv == out && n != 1) return fail(DL_E_ARG, "dl_q8_reduce: in place needs n_peers == 1");
+  hipError_t e = dl::launch_q8_reduce(static_cast<const uint8_t*>(recv), n, m, divisor,
+                                      static_cast<uint8_t*>(out), static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_q8_reduce");
+}
+
+DL_API int dl_unpack_sgd_q8(dl_tree_t t, int32_t b, const void* slots, float* outer, float* mom,
+                            float lr, float momentum, int32_t nesterov, int32_t first_step,
+                            int32_t inner_slot, dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd_q8", kAutoUnpackSgd));
+  DL_TRY(check_packed(slots, "dl_unpack_sgd_q8", "slots"));
+  DL_TRY(check_packed(outer, "dl_unpack_sgd_q8", "outer"));
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_unpack_sgd_q8", "momentum"));
+  DL_TRY(check_slot(t, inner_slot, "dl_unpack_sgd_q8", true));
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_unpack_sgd_q8: Nesterov momentum requires a momentum");
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_unpack_sgd_q8(L, static_cast<const uint8_t*>(slots), outer, mom, a,
+                                          inner_slot);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_unpack_sgd_q8");
 }
 
 DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int32_t dtype,

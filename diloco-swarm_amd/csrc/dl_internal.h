@@ -48,6 +48,11 @@ hipError_t launch_unpack_avg(const Launch& L, const void* wire, int wire_dtype, 
 hipError_t launch_unpack_sgd(const Launch& L, const void* wire, int wire_dtype, int divisor,
                              float* outer, float* mom, SgdArgs a, int inner_slot);
 hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float* mom, SgdArgs a);
+hipError_t launch_delta_q8(const Launch& L, int inner_slot, const float* outer, uint8_t* slots);
+hipError_t launch_unpack_sgd_q8(const Launch& L, const uint8_t* slots, float* outer, float* mom,
+                                SgdArgs a, int inner_slot);
+hipError_t launch_q8_reduce(const uint8_t* recv, int32_t n, int32_t m, int32_t divisor,
+                            uint8_t* out, hipStream_t s);
 hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype);
 hipError_t launch_scatter(const Launch& L, const float* packed, int dst_slot);
 hipError_t launch_serialize(const void* src, int src_dtype, int64_t numel, float m0, float m1,

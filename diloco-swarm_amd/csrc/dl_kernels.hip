@@ -17,126 +17,10 @@
 //                u   = fma(buf, m, g)   (grad.add(buf, alpha=m): CPU fmadd)
 //                θ   = fma(u, -lr, θ)   (param.add_(grad, alpha=-lr))
 //   copy-back  : inner = θ                              (src/utils.py:226)
-#include "dl_internal.h"
+#include "dl_device.h"
 
 namespace dl {
 namespace {
-
-__device__ __forceinline__ bool aligned16(const void* p) {
-  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
-}
-
-// ---- element types on the wire / in packed buffers -----------------------------------------
-__device__ __forceinline__ uint16_t f2bf(float x) {
-  __bf16 b = static_cast<__bf16>(x);  // v_cvt_pk_bf16_f32: RNE, NaN stays NaN
-  return __builtin_bit_cast(uint16_t, b);
-}
-__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
-__device__ __forceinline__ float h2f(uint16_t h) {
-  return static_cast<float>(__builtin_bit_cast(_Float16, h));
-}
-
-struct bf16_t {
-  uint16_t bits;
-};
-
-// Streaming memory ops. NT = non-temporal (`global_load/store_dwordx4 ... nt`): the operands
-// are touched once per outer step and are larger than the 256 MiB Infinity Cache, so keeping
-// them out of the caches measured +10-15 % on streaming loads (tools/hbm_bench.hip,
-// DESIGN.md "Kernels"). Whether stores are NT is a per-tree tuning flag (dl_tree_tune).
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-// Pointers from the device pointer table are generic (flat) to the compiler; casting to the
-// global address space turns flat_load/store (counted on vmcnt AND lgkmcnt, completed out of
-// order) into global_load/store.
-#define DL_GLOBAL __attribute__((address_space(1)))
-typedef DL_GLOBAL const f32x4* gcf4;
-typedef DL_GLOBAL f32x4* gf4;
-typedef DL_GLOBAL const uint64_t* gcu64;
-typedef DL_GLOBAL uint64_t* gu64;
-
-template <bool NT>
-__device__ __forceinline__ float4 ldf4(const float* p, int v) {
-  gcf4 q = (gcf4)(p) + v;
-  f32x4 r;
-  if constexpr (NT) r = __builtin_nontemporal_load(q);
-  else r = *q;
-  return make_float4(r.x, r.y, r.z, r.w);
-}
-template <bool NT>
-__device__ __forceinline__ void stf4(float* p, int v, float4 x) {
-  gf4 q = (gf4)(p) + v;
-  const f32x4 r = {x.x, x.y, x.z, x.w};
-  if constexpr (NT) __builtin_nontemporal_store(r, q);
-  else *q = r;
-}
-template <bool NT>
-__device__ __forceinline__ uint64_t ld8(const void* p, int v) {
-  gcu64 q = (gcu64)(p) + v;
-  if constexpr (NT) return __builtin_nontemporal_load(q);
-  else return *q;
-}
-template <bool NT>
-__device__ __forceinline__ void st8(void* p, int v, uint64_t x) {
-  gu64 q = (gu64)(p) + v;
-  if constexpr (NT) __builtin_nontemporal_store(x, q);
-  else *q = x;
-}
-
-template <typename W>
-struct WireIO;
-
-template <>
-struct WireIO<float> {
-  template <bool NT>
-  static __device__ __forceinline__ float4 ld4(const float* p, int v) { return ldf4<NT>(p, v); }
-  template <bool NT>
-  static __device__ __forceinline__ void st4(float* p, int v, float4 x) { stf4<NT>(p, v, x); }
-  static __device__ __forceinline__ float ld1(const float* p, int i) { return p[i]; }
-  static __device__ __forceinline__ void st1(float* p, int i, float x) { p[i] = x; }
-};
-
-template <>
-struct WireIO<bf16_t> {
-  template <bool NT>
-  static __device__ __forceinline__ float4 ld4(const bf16_t* p, int v) {
-    const uint64_t r = ld8<NT>(p, v);
-    return make_float4(bf2f(uint16_t(r)), bf2f(uint16_t(r >> 16)), bf2f(uint16_t(r >> 32)),
-                       bf2f(uint16_t(r >> 48)));
-  }
-  template <bool NT>
-  static __device__ __forceinline__ void st4(bf16_t* p, int v, float4 x) {
-    const uint64_t r = uint64_t(f2bf(x.x)) | (uint64_t(f2bf(x.y)) << 16) |
-                       (uint64_t(f2bf(x.z)) << 32) | (uint64_t(f2bf(x.w)) << 48);
-    st8<NT>(p, v, r);
-  }
-  static __device__ __forceinline__ float ld1(const bf16_t* p, int i) { return bf2f(p[i].bits); }
-  static __device__ __forceinline__ void st1(bf16_t* p, int i, float x) { p[i].bits = f2bf(x); }
-};
-
-
-__device__ __forceinline__ float4 sub4(float4 a, float4 b) {
-  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
-}
-__device__ __forceinline__ float4 div4(float4 a, float d) {
-  return make_float4(a.x / d, a.y / d, a.z / d, a.w / d);
-}
-
-template <typename T>
-__device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot, int c) {
-  return static_cast<T*>(caddr[slot * nchunk + c]);
-}
-
-// ---- the walker ----------------------------------------------------------------------------
-// Body::operator() is instantiated per (NTL, NTS) policy: non-temporal loads / stores.
-template <class Body, bool NTL, bool NTS>
-__global__ void __launch_bounds__(kThreads)
-    k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ caddr,
-           int32_t nchunk, Body body) {
-  for (int32_t c = c0 + int32_t(blockIdx.x); c < c1; c += int32_t(gridDim.x)) {
-    const Chunk ck = chunks[c];
-    body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x));
-  }
-}
 
 // a2: wire = outer - inner
 template <typename W>
@@ -210,18 +94,6 @@ struct UnpackAvg {
     }
   }
 };
-
-// a3+a4+a5 fused. MODE 0: momentum 0; 1: first step (buf = g); 2: buf = buf*m + g.
-template <int MODE>
-__device__ __forceinline__ void sgd1(float g, float& buf, float& th, const SgdArgs& a) {
-  if (MODE == 0) {
-    th = __builtin_fmaf(g, a.neg_lr, th);
-  } else {
-    buf = (MODE == 1) ? g : (buf * a.momentum) + g;  // contract off: two roundings
-    const float u = a.nesterov ? __builtin_fmaf(buf, a.momentum, g) : buf;
-    th = __builtin_fmaf(u, a.neg_lr, th);
-  }
-}
 
 template <typename W, bool DIV, int MODE>
 struct UnpackSgd {
@@ -407,25 +279,6 @@ struct Scatter {
     }
   }
 };
-
-template <class Body, bool NTL, bool NTS>
-hipError_t run_policy(const Launch& L, const Body& body, int32_t grid) {
-  hipLaunchKernelGGL((k_walk<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream, L.chunks,
-                     L.c0, L.c1, L.caddr, L.nchunk, body);
-  return hipGetLastError();
-}
-
-template <class Body>
-hipError_t run(const Launch& L, const Body& body) {
-  const int32_t n = L.c1 - L.c0;
-  if (n <= 0) return hipSuccess;
-  const int32_t grid = (L.grid > 0 && L.grid < n) ? L.grid : n;  // default: one workgroup per chunk
-  const bool ntl = (L.flags & DL_TUNE_NT_LOADS) != 0, nts = (L.flags & DL_TUNE_NT_STORES) != 0;
-  if (ntl && nts) return run_policy<Body, true, true>(L, body, grid);
-  if (ntl) return run_policy<Body, true, false>(L, body, grid);
-  if (nts) return run_policy<Body, false, true>(L, body, grid);
-  return run_policy<Body, false, false>(L, body, grid);
-}
 
 // ---- serializer and synthetic fill -----------------------------------------------------------
 template <typename S>

@@ -20,6 +20,7 @@ ALIGN_ELEMS = 64
 CHUNK_ELEMS = 4096
 ALL_BUCKETS = -1
 MAX_SLOTS = 4
+Q8_SLOT_BYTES = 4160
 DL_F32, DL_BF16, DL_F16 = 0, 1, 2
 TUNE_NT_LOADS, TUNE_NT_STORES = 1, 2
 TUNE_AUTO = -1
@@ -38,6 +39,7 @@ SIGNATURES = {
     "dl_tree_query": (ctypes.c_int, [_vp, _pi64, _pi32, _pi32, _pi32]),
     "dl_tree_bucket_range": (ctypes.c_int, [_vp, _i32, _pi64, _pi64]),
     "dl_tree_seg_off": (ctypes.c_int, [_vp, _pi64]),
+    "dl_tree_bucket_chunks": (ctypes.c_int, [_vp, _i32, _pi32, _pi32]),
     "dl_tree_bind": (ctypes.c_int, [_vp, _i32, _pu64, _i32, _vp]),
     "dl_tree_tune": (ctypes.c_int, [_vp, _i32, _i32]),
     "dl_delta_pack": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _vp]),
@@ -47,6 +49,11 @@ SIGNATURES = {
         [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _i32, _vp],
     ),
     "dl_delta_sgd": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _vp]),
+    "dl_delta_q8": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
+    "dl_q8_reduce": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _vp]),
+    "dl_unpack_sgd_q8": (
+        ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _f32, _f32, _i32, _i32, _i32, _vp],
+    ),
     "dl_gather": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp]),
     "dl_scatter": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp]),
     "dl_serialize": (ctypes.c_int, [_vp, _i32, _i64, _f32, _f32, _vp, _vp]),

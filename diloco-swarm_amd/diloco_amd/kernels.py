@@ -17,6 +17,9 @@ from .plan import DEFAULT_BUCKET_CAP_ELEMS, PackedTree
 _DT = {torch.float32: _lib.DL_F32, torch.bfloat16: _lib.DL_BF16}
 
 
+Q8_SLOT = _lib.Q8_SLOT_BYTES
+
+
 def wire_code(dtype: torch.dtype) -> int:
     try:
         return _DT[dtype]
@@ -65,6 +68,21 @@ class HipKernels:
                   first) -> None:
         _lib.call("dl_delta_sgd", tree.handle, bucket, inner_slot, theta.data_ptr(), _ptr(mom),
                   float(lr), float(momentum), int(nesterov), int(first), _s(theta))
+
+    # int8 wire codec (DL_Q8_SLOT_BYTES slots, one per chunk)
+    def delta_q8(self, tree, bucket, inner_slot, theta, slots) -> None:
+        _lib.call("dl_delta_q8", tree.handle, bucket, inner_slot, theta.data_ptr(),
+                  slots.data_ptr(), _s(theta))
+
+    def q8_reduce(self, recv, n_peers, n_slots, divisor, out) -> None:
+        _lib.call("dl_q8_reduce", recv.data_ptr(), int(n_peers), int(n_slots), int(divisor),
+                  out.data_ptr(), _s(out))
+
+    def unpack_sgd_q8(self, tree, bucket, slots, theta, mom, lr, momentum, nesterov, first,
+                      inner_slot) -> None:
+        _lib.call("dl_unpack_sgd_q8", tree.handle, bucket, slots.data_ptr(), theta.data_ptr(),
+                  _ptr(mom), float(lr), float(momentum), int(nesterov), int(first),
+                  int(inner_slot), _s(theta))
 
     def unpack_avg(self, tree, bucket, wire, divisor, dst_slot, dst_packed=None) -> None:
         _lib.call("dl_unpack_avg", tree.handle, bucket, wire.data_ptr(), wire_code(wire.dtype),

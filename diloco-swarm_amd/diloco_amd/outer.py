@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .kernels import default_kernels
+from .kernels import Q8_SLOT, default_kernels
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER
 
 ALL = _lib.ALL_BUCKETS
@@ -94,7 +94,25 @@ class OuterSync:
         self.theta = torch.zeros(self.tree.total, dtype=torch.float32, **z)
         self.mom = (torch.zeros(self.tree.total, dtype=torch.float32, **z)
                     if self.momentum != 0 else None)
-        self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, **z)
+        if wire_dtype not in (torch.float32, torch.bfloat16, torch.int8):
+            raise ValueError(f"wire dtype {wire_dtype}: float32, bfloat16 or int8")
+        self.q8 = wire_dtype == torch.int8
+        if self.q8:
+            # int8 codec: one Q8_SLOT-byte slot per chunk; bucket b's slots padded to a
+            # multiple of the peer count so both exchanges split evenly (dl_q8.hip)
+            n = self.world_size
+            self.q8_plan, base, mmax = [], 0, 1
+            for c0, c1 in self.tree.bucket_chunks:
+                m = max(1, -(-(c1 - c0) // n))
+                self.q8_plan.append((c1 - c0, m, base))
+                base += n * m
+                mmax = max(mmax, m)
+            self.wire = None
+            self.q_slots = torch.zeros(base * Q8_SLOT, dtype=torch.uint8, **z)
+            self.q_recv = torch.zeros(n * mmax * Q8_SLOT, dtype=torch.uint8, **z)
+            self.q_red = torch.zeros(mmax * Q8_SLOT, dtype=torch.uint8, **z)
+        else:
+            self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, **z)
         self.k.gather(self.tree, ALL, SLOT_INNER, self.theta)
         self.steps_done = 0
         # step() runs on its own stream, ordered after the caller's current stream and joined
@@ -106,9 +124,33 @@ class OuterSync:
 
     # ---- building blocks (each stream-ordered on the current stream) ----------------------
     def pseudo_gradient(self, bucket: int = ALL) -> None:
-        """wire[bucket] = θ_outer - inner (a2)."""
+        """wire[bucket] = θ_outer - inner (a2); int8 wire: its quantised slots."""
         self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
-        self.k.delta_pack(self.tree, bucket, SLOT_INNER, self.theta, self.wire)
+        if self.q8:
+            self.k.delta_q8(self.tree, bucket, SLOT_INNER, self.theta, self.q8_region(bucket))
+        else:
+            self.k.delta_pack(self.tree, bucket, SLOT_INNER, self.theta, self.wire)
+
+    def q8_region(self, bucket: int) -> torch.Tensor:
+        """The int8 slots of one bucket (n * m slots, chunk order, zero padding at the end)."""
+        if bucket == ALL:
+            if self.tree.n_buckets != 1:
+                raise ValueError("the int8 wire works bucket by bucket")
+            bucket = 0
+        _nch, m, base = self.q8_plan[bucket]
+        return self.q_slots[base * Q8_SLOT:(base + self.world_size * m) * Q8_SLOT]
+
+    def q8_exchange(self, bucket: int):
+        """all_to_all -> dl_q8_reduce (Σ_r in rank order, / n, re-quantise) -> async all_gather
+        of the averaged slots back into the bucket's region; returns the all_gather handle."""
+        _nch, m, _base = self.q8_plan[bucket]
+        n = self.world_size
+        region = self.q8_region(bucket)
+        recv = self.q_recv[:n * m * Q8_SLOT]
+        dist.all_to_all_single(recv, region, group=self.group, async_op=True).wait()
+        red = self.q_red[:m * Q8_SLOT]
+        self.k.q8_reduce(recv, n, m, n, red)
+        return dist.all_gather_into_tensor(region, red, group=self.group, async_op=True)
 
     def bucket_view(self, bucket: int) -> torch.Tensor:
         if bucket == ALL:
@@ -123,9 +165,14 @@ class OuterSync:
 
     def apply(self, bucket: int = ALL, write_inner: bool = True) -> None:
         """g = wire/n; Nesterov SGD on θ_outer; inner = θ_outer (a3 /n, a4, a5)."""
+        slot = SLOT_INNER if write_inner else -1
+        if self.q8:  # the slots already hold the average
+            self.k.unpack_sgd_q8(self.tree, bucket, self.q8_region(bucket), self.theta, self.mom,
+                                 self.lr, self.momentum, self.nesterov, self.steps_done == 0,
+                                 slot)
+            return
         self.k.unpack_sgd(self.tree, bucket, self.wire, self.world_size, self.theta, self.mom,
-                          self.lr, self.momentum, self.nesterov, self.steps_done == 0,
-                          SLOT_INNER if write_inner else -1)
+                          self.lr, self.momentum, self.nesterov, self.steps_done == 0, slot)
 
     # ---- the outer step ---------------------------------------------------------------------
     def step(self, pipeline: Optional[bool] = None) -> None:
@@ -145,7 +192,9 @@ class OuterSync:
     def _step(self, pipeline: Optional[bool]) -> None:
         if pipeline is None:
             pipeline = self.world_size > 1
-        if pipeline:
+        if self.q8:
+            self._step_q8(pipeline)
+        elif pipeline:
             pipelined_buckets(self.tree.n_buckets, self.pseudo_gradient,
                               lambda b: self.all_reduce(b, async_op=True), self.apply)
         elif self.fuse_single:
@@ -157,6 +206,25 @@ class OuterSync:
             self.pseudo_gradient(ALL)
             self.apply(ALL)
         self.steps_done += 1
+
+    def _step_q8(self, pipeline: bool) -> None:
+        nb = self.tree.n_buckets
+        if not pipeline:  # one replica: the average of one is its own re-quantised slots
+            for b in range(nb):
+                self.pseudo_gradient(b)
+                nch, m, _ = self.q8_plan[b]
+                region = self.q8_region(b)
+                self.k.q8_reduce(region, 1, m, 1, region)
+                self.apply(b)
+            return
+        # pack(b+1) and its all_to_all overlap all_gather(b) and unpack(b)
+        self.pseudo_gradient(0)
+        for b in range(nb):
+            gather = self.q8_exchange(b)
+            if b + 1 < nb:
+                self.pseudo_gradient(b + 1)
+            gather.wait()
+            self.apply(b)
 
     def unpacked(self, packed: torch.Tensor) -> List[torch.Tensor]:
         """Per-tensor views into a packed buffer (shapes of the inner params)."""

@@ -62,10 +62,14 @@ class PackedTree:
         _lib.call("dl_tree_seg_off", h, seg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
         self.seg_off = seg
         self.bucket_ranges: List[Tuple[int, int]] = []
+        self.bucket_chunks: List[Tuple[int, int]] = []
         for b in range(self.n_buckets):
             lo, hi = ctypes.c_int64(), ctypes.c_int64()
             _lib.call("dl_tree_bucket_range", h, b, ctypes.byref(lo), ctypes.byref(hi))
             self.bucket_ranges.append((lo.value, hi.value))
+            c0, c1 = ctypes.c_int32(), ctypes.c_int32()
+            _lib.call("dl_tree_bucket_chunks", h, b, ctypes.byref(c0), ctypes.byref(c1))
+            self.bucket_chunks.append((c0.value, c1.value))
         self._bound = [None] * _lib.MAX_SLOTS
 
     @property

@@ -35,6 +35,7 @@ extern "C" {
 #define DL_CHUNK_ELEMS 4096    /* work unit of every segment walker: 16 KiB of fp32 */
 #define DL_ALL_BUCKETS (-1)
 #define DL_MAX_SLOTS 4         /* per-tensor pointer tables per tree */
+#define DL_Q8_SLOT_BYTES 4160  /* int8 wire: 64-B header (fp32 scale) + DL_CHUNK_ELEMS int8 */
 
 /* wire / packed dtypes */
 #define DL_F32 0
@@ -72,6 +73,9 @@ DL_API int dl_tree_query(dl_tree_t tree, int64_t* total_elems, int32_t* n_seg, i
 DL_API int dl_tree_bucket_range(dl_tree_t tree, int32_t bucket, int64_t* elem_begin,
                                 int64_t* elem_end);
 DL_API int dl_tree_seg_off(dl_tree_t tree, int64_t* seg_off /* n_seg+1 */);
+/* Chunk index range [chunk_begin, chunk_end) of a bucket (DL_ALL_BUCKETS: the whole tree). */
+DL_API int dl_tree_bucket_chunks(dl_tree_t tree, int32_t bucket, int32_t* chunk_begin,
+                                 int32_t* chunk_end);
 /* Upload the device addresses of the n_seg tensors of one slot (e.g. inner params, grads).
  * fp32 tensors, contiguous; a 16-B-misaligned address takes the scalar path. Synchronises
  * `stream` once (pointer sets change rarely; call again only when addresses change). */
@@ -132,6 +136,23 @@ DL_API int dl_gather(dl_tree_t tree, int32_t bucket, int32_t src_slot, void* pac
 /* a5: sync_inner_model, src/utils.py:223-226: dst[seg][j] = packed[k] (fp32). */
 DL_API int dl_scatter(dl_tree_t tree, int32_t bucket, const float* packed, int32_t dst_slot,
                       dl_stream_t stream);
+
+/* ---- int8 wire codec (not in the reference) --------------------------
+ * One DL_Q8_SLOT_BYTES slot per chunk of the bucket, in chunk order: fp32 scale at byte 0,
+ * int8 values at byte 64 (bytes past the chunk's length stay zero; slots must be zeroed once).
+ * Quantiser: s = amax/127, q = s == 0 ? 0 : clamp(rint(x/s), -127, 127), value q*s.
+ * dl_delta_q8:      slots <- quantise(outer - inner) per chunk  (a2, 8 B read + 1.02 B written)
+ * dl_q8_reduce:     out[j] <- quantise((sum_r deq(recv[r][j])) / divisor), r in rank order;
+ *                   recv holds n_peers x n_slots slots; out may alias recv when n_peers == 1
+ * dl_unpack_sgd_q8: g = deq(slot); SGD and copy-back exactly as dl_unpack_sgd (divisor 1). */
+DL_API int dl_delta_q8(dl_tree_t tree, int32_t bucket, int32_t inner_slot,
+                       const float* outer_packed, void* slots, dl_stream_t stream);
+DL_API int dl_q8_reduce(const void* recv, int32_t n_peers, int32_t n_slots, int32_t divisor,
+                        void* out, dl_stream_t stream);
+DL_API int dl_unpack_sgd_q8(dl_tree_t tree, int32_t bucket, const void* slots,
+                            float* outer_packed, float* mom_packed, float lr, float momentum,
+                            int32_t nesterov, int32_t first_step, int32_t inner_slot,
+                            dl_stream_t stream);
 
 /* ---- serializer (src/serializer.py:11-15) ----------------------------------------------
  * out is fp32 of 2*numel elements: out[0] = meta0, out[1] = meta1, out[numel + i] =

@@ -116,3 +116,52 @@ OR_API void or_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream,
     dst[i] = x;
   }
 }
+
+/* ---- int8 wire codec (the build's own codec; restates dl_q8.hip) ------
+ * Slot = 64-B header (fp32 scale at byte 0) + 4096 int8 values; s = amax/127,
+ * q = s == 0 ? 0 : clamp(rint(x/s), -127, 127); dequantised value q*s. */
+#define OR_Q8_HDR 64
+#define OR_Q8_SLOT 4160
+#define OR_CHUNK 4096
+
+static int8_t or_q8(float x, float s) {
+  if (s == 0.0f) return 0;
+  return (int8_t)(int)fminf(fmaxf(rintf(x / s), -127.0f), 127.0f);
+}
+
+static void or_quantize(const float* x, int64_t len, uint8_t* slot) {
+  float am = 0.0f;
+  for (int64_t i = 0; i < len; ++i) am = fmaxf(am, fabsf(x[i]));
+  const float s = am / 127.0f;
+  memcpy(slot, &s, 4);
+  for (int64_t i = 0; i < len; ++i) slot[OR_Q8_HDR + i] = (uint8_t)or_q8(x[i], s);
+}
+
+/* one chunk: slot <- quantise(outer - inner); bytes past len untouched */
+OR_API void or_delta_q8(const float* outer, const float* inner, int64_t len, uint8_t* slot) {
+  float d[OR_CHUNK];
+  for (int64_t i = 0; i < len; ++i) d[i] = outer[i] - inner[i];
+  or_quantize(d, len, slot);
+}
+
+OR_API void or_q8_deq(const uint8_t* slot, int64_t len, float* out) {
+  float s;
+  memcpy(&s, slot, 4);
+  for (int64_t i = 0; i < len; ++i) out[i] = (float)(int8_t)slot[OR_Q8_HDR + i] * s;
+}
+
+/* out[j] <- quantise((sum_{r<n} deq(recv[r*m + j])) / divisor), over all 4096 values */
+OR_API void or_q8_reduce(const uint8_t* recv, int32_t n, int32_t m, int32_t divisor,
+                         uint8_t* out) {
+  float acc[OR_CHUNK], x[OR_CHUNK];
+  for (int32_t j = 0; j < m; ++j) {
+    for (int i = 0; i < OR_CHUNK; ++i) acc[i] = 0.0f;
+    for (int32_t r = 0; r < n; ++r) {
+      or_q8_deq(recv + ((int64_t)r * m + j) * OR_Q8_SLOT, OR_CHUNK, x);
+      for (int i = 0; i < OR_CHUNK; ++i) acc[i] = acc[i] + x[i];
+    }
+    if (divisor > 1)
+      for (int i = 0; i < OR_CHUNK; ++i) acc[i] = acc[i] / (float)divisor;
+    or_quantize(acc, OR_CHUNK, out + (int64_t)j * OR_Q8_SLOT);
+  }
+}

@@ -49,7 +49,12 @@ def load():
         lib.or_bf16_round.argtypes = [_F, _F, ctypes.c_int64]
         lib.or_fill_synth.argtypes = [_F, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64,
                                       ctypes.c_float, ctypes.c_float, _F]
-        for f in ("or_delta", "or_sum_avg", "or_sgd", "or_copy", "or_bf16_round", "or_fill_synth"):
+        _U8 = ctypes.POINTER(ctypes.c_uint8)
+        lib.or_delta_q8.argtypes = [_F, _F, ctypes.c_int64, _U8]
+        lib.or_q8_deq.argtypes = [_U8, ctypes.c_int64, _F]
+        lib.or_q8_reduce.argtypes = [_U8, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _U8]
+        for f in ("or_delta", "or_sum_avg", "or_sgd", "or_copy", "or_bf16_round", "or_fill_synth",
+                  "or_delta_q8", "or_q8_deq", "or_q8_reduce"):
             getattr(lib, f).restype = None
         _lib = lib
     return _lib
@@ -125,6 +130,82 @@ def fill_synth(n: int, seed: int, stream: int, base: float, scale: float, add=No
     load().or_fill_synth(_fp(out), n, seed, stream, base, scale,
                          _fp(add) if add is not None else None)
     return out
+
+
+# ---- int8 wire codec ------------------------------------------------------------------------
+Q8_SLOT, Q8_HDR, CHUNK = 4160, 64, 4096
+
+
+def _u8(a: np.ndarray):
+    assert a.dtype == np.uint8 and a.flags.c_contiguous
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def chunks_of(numel: int):
+    """(offset, length) of each DL_CHUNK_ELEMS chunk of one tensor, in order."""
+    return [(o, min(CHUNK, numel - o)) for o in range(0, numel, CHUNK)]
+
+
+def delta_q8(outer: np.ndarray, inner: np.ndarray) -> np.ndarray:
+    """Slots (one per chunk) of quantise(outer - inner) for one tensor."""
+    ch = chunks_of(outer.size)
+    slots = np.zeros(len(ch) * Q8_SLOT, dtype=np.uint8)
+    for k, (o, n) in enumerate(ch):
+        load().or_delta_q8(_fp(np.ascontiguousarray(outer[o:o + n])),
+                           _fp(np.ascontiguousarray(inner[o:o + n])), n,
+                           _u8(slots[k * Q8_SLOT:(k + 1) * Q8_SLOT]))
+    return slots
+
+
+def q8_reduce(recv: np.ndarray, n: int, m: int, divisor: int) -> np.ndarray:
+    out = np.zeros(m * Q8_SLOT, dtype=np.uint8)
+    load().or_q8_reduce(_u8(np.ascontiguousarray(recv)), n, m, divisor, _u8(out))
+    return out
+
+
+def q8_deq(slots: np.ndarray, numel: int) -> np.ndarray:
+    out = np.empty(numel, dtype=np.float32)
+    for k, (o, n) in enumerate(chunks_of(numel)):
+        buf = np.empty(n, dtype=np.float32)
+        load().or_q8_deq(_u8(np.ascontiguousarray(slots[k * Q8_SLOT:(k + 1) * Q8_SLOT])), n,
+                         _fp(buf))
+        out[o:o + n] = buf
+    return out
+
+
+def q8_average(deltas_by_rank, numels, bucket_chunks):
+    """The int8 exchange of one outer step, restated: per-tensor deltas of every rank ->
+    per-tensor averaged, dequantised g (what every rank applies). bucket_chunks: list of
+    chunk counts per bucket (chunks in tree order)."""
+    n = len(deltas_by_rank)
+    slots = [np.concatenate([delta_q8_from(d[t]) for t in range(len(numels))])
+             for d in deltas_by_rank]
+    avg_slots, c = [], 0
+    for nch in bucket_chunks:
+        m = -(-nch // n)
+        per = []
+        for r in range(n):
+            s = np.zeros(n * m * Q8_SLOT, dtype=np.uint8)
+            s[:nch * Q8_SLOT] = slots[r][c * Q8_SLOT:(c + nch) * Q8_SLOT]
+            per.append(s)
+        gathered = []
+        for p in range(n):  # all_to_all: peer p gets slots [p*m, (p+1)*m) from every rank
+            recv = np.concatenate([per[r][p * m * Q8_SLOT:(p + 1) * m * Q8_SLOT] for r in range(n)])
+            gathered.append(q8_reduce(recv, n, m, n))
+        avg_slots.append(np.concatenate(gathered)[:nch * Q8_SLOT])  # all_gather, drop padding
+        c += nch
+    flat = np.concatenate(avg_slots)
+    out, c = [], 0
+    for t, numel in enumerate(numels):
+        k = len(chunks_of(numel))
+        out.append(q8_deq(flat[c * Q8_SLOT:(c + k) * Q8_SLOT], numel))
+        c += k
+    return out
+
+
+def delta_q8_from(delta: np.ndarray) -> np.ndarray:
+    """Slots of quantise(delta) for one tensor (delta = outer - inner already formed)."""
+    return delta_q8(delta, np.zeros_like(delta))
 
 
 # ---- one outer step over a tree ----------------------------------------------------------

@@ -25,6 +25,14 @@ class CpuTree:
         self.n_chunks = 0
         self.bucket_ranges = [(int(seg[bnd[b]]), int(seg[bnd[b + 1]])) for b in range(self.n_buckets)]
         self.slots = {}
+        # chunk table in tree order: (seg, offset in tensor, length, packed offset)
+        self.chunks, self.bucket_chunks = [], []
+        for b in range(self.n_buckets):
+            c0 = len(self.chunks)
+            for i in range(int(bnd[b]), int(bnd[b + 1])):
+                for o, n in oracle.chunks_of(self.numels[i]):
+                    self.chunks.append((i, o, n, int(seg[i]) + o))
+            self.bucket_chunks.append((c0, len(self.chunks)))
 
     def segs(self, bucket):
         if bucket == -1:
@@ -89,6 +97,42 @@ class OracleKernels:
             if mom is not None:
                 self._seg(tree, mom, i)[:] = b
             inner[:] = th
+
+    def _chunk_range(self, tree, bucket):
+        return (0, len(tree.chunks)) if bucket == -1 else tree.bucket_chunks[bucket]
+
+    def delta_q8(self, tree, bucket, inner_slot, theta, slots):
+        c0, c1 = self._chunk_range(tree, bucket)
+        th, q = _np(theta), _np(slots)
+        for c in range(c0, c1):
+            seg, o, n, po = tree.chunks[c]
+            inner = _np(tree.slots[inner_slot][seg])[o:o + n]
+            j = (c - c0) * oracle.Q8_SLOT
+            oracle.load().or_delta_q8(oracle._fp(np.ascontiguousarray(th[po:po + n])),
+                                      oracle._fp(np.ascontiguousarray(inner)), n,
+                                      oracle._u8(q[j:j + oracle.Q8_SLOT]))
+
+    def q8_reduce(self, recv, n_peers, n_slots, divisor, out):
+        res = oracle.q8_reduce(_np(recv).copy(), n_peers, n_slots, divisor)
+        _np(out)[:res.size] = res
+
+    def unpack_sgd_q8(self, tree, bucket, slots, theta, mom, lr, momentum, nesterov, first,
+                      inner_slot):
+        c0, c1 = self._chunk_range(tree, bucket)
+        q = _np(slots)
+        for c in range(c0, c1):
+            seg, o, n, po = tree.chunks[c]
+            j = (c - c0) * oracle.Q8_SLOT
+            g = np.empty(n, dtype=np.float32)
+            oracle.load().or_q8_deq(oracle._u8(q[j:j + oracle.Q8_SLOT]), n, oracle._fp(g))
+            th = _np(theta)[po:po + n].copy()
+            b = _np(mom)[po:po + n].copy() if mom is not None else None
+            oracle.sgd(th, b, g, lr, momentum, nesterov, first)
+            _np(theta)[po:po + n] = th
+            if mom is not None:
+                _np(mom)[po:po + n] = b
+            if inner_slot >= 0:
+                _np(tree.slots[inner_slot][seg])[o:o + n] = th
 
     def unpack_avg(self, tree, bucket, wire, divisor, dst_slot, dst_packed=None):
         for i in tree.segs(bucket):

@@ -18,7 +18,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN, PKG, REPO, load_npz, normwise_ok, split
+from conftest import PKG, REPO, load_npz, normwise_ok, split
+from expect import MICRO_Q8_CAP, expected_q8
 
 MICRO_STEPS = 2
 # stand-in for src/metrics.py Outputs (a pydantic model there); module level so it pickles
@@ -104,6 +105,20 @@ def _worker(rank, world, port, mode, num_stages, out):
             eng.step()
             rec[f"theta_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(eng.theta)])
             rec[f"buf_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(eng.mom)])
+            rec[f"inner_s{s}"] = np.concatenate([p.numpy().reshape(-1) for p in params])
+    elif mode == "engine_q8":
+        params = [torch.from_numpy(v.copy()) for v in theta0]
+        eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=torch.int8,
+                        group=world_.curr_stage_group, world_size=len(world_.dp_ranks),
+                        bucket_cap_elems=MICRO_Q8_CAP)
+        assert eng.tree.n_buckets > 2
+        for s in range(1, MICRO_STEPS + 1):
+            th = eng.unpacked(eng.theta)
+            vals = synth.inner_tree([t.numpy().reshape(-1) for t in th], s, dp_rank)
+            for p, v in zip(params, vals):
+                p.copy_(torch.from_numpy(v))
+            eng.step()
+            rec[f"theta_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(eng.theta)])
             rec[f"inner_s{s}"] = np.concatenate([p.numpy().reshape(-1) for p in params])
     elif mode == "gradsync":
         from diloco_amd.gradsync import GradSync
@@ -196,3 +211,18 @@ def test_sync_outputs_aggregates_like_reference():
     # norm mean(0.5, 0.5)
     assert recs[0]["agg"].tolist() == [300, 1, 1.5, 2.0, 0.5]
     assert recs[1]["agg"].tolist() == recs[0]["agg"].tolist()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_int8_wire_exchange_matches_oracle(world):
+    """all_to_all -> rank-order reduce -> all_gather over a real process group: every replica
+    ends bit-identical to the oracle's restatement of the codec (deterministic at any n)."""
+    exp = expected_q8(world)
+    for rec in _run("engine_q8", world):
+        for s in (1, 2):
+            assert rec[f"theta_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), s
+            assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), s
+    # and the codec is close to the exact fp32 average
+    g = load_npz(f"micro_n{world}.npz")
+    err = np.abs(exp["theta_s1"] - g["theta_s1"]).max() / np.abs(g["theta_s1"] - g["theta0"]).max()
+    assert err < 2e-2

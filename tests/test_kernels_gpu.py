@@ -323,3 +323,88 @@ def test_t13b_full_size_sampled_tensors_vs_oracle_and_fused():
         assert got.tobytes() == st.theta[0].tobytes(), t
     ea.close()
     eb.close()
+
+
+# ---- int8 wire codec -----------------------------------------------------
+def _q8_emulated_step(engines, inners, step):
+    """n int8-wire replicas on one GPU: all_to_all / all_gather emulated with copies, the
+    reduce is the product kernel (dl_q8_reduce)."""
+    from diloco_amd.kernels import Q8_SLOT
+
+    n = len(engines)
+    for r, (e, inner) in enumerate(zip(engines, inners)):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, step, r, out=[p.view(-1) for p in inner])
+    for b in range(engines[0].tree.n_buckets):
+        for e in engines:
+            e.pseudo_gradient(b)
+        _nch, m, _ = engines[0].q8_plan[b]
+        regions = [e.q8_region(b) for e in engines]
+        outs = []
+        for p, e in enumerate(engines):  # peer p reduces slots [p*m, (p+1)*m) of every replica
+            recv = torch.cat([reg[p * m * Q8_SLOT:(p + 1) * m * Q8_SLOT] for reg in regions])
+            out = torch.zeros(m * Q8_SLOT, dtype=torch.uint8, device=DEV)
+            e.k.q8_reduce(recv, n, m, n, out)
+            outs.append(out)
+        gathered = torch.cat(outs)
+        for reg in regions:
+            reg.copy_(gathered)
+        for e in engines:
+            e.apply(b)
+    for e in engines:
+        e.steps_done += 1
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_int8_wire_matches_oracle_restatement(n):
+    from expect import MICRO_Q8_CAP, expected_q8
+
+    exp = expected_q8(n)
+    spec = get_tree("micro")
+    theta0 = synth.outer_tree_device(spec, DEV)
+    shapes = [s for _, s in spec.params()]
+    engines, inners = [], []
+    for _ in range(n):
+        inner = [t.clone().view(s) for t, s in zip(theta0, shapes)]
+        engines.append(OuterSync(inner, world_size=n, wire_dtype=torch.int8,
+                                 bucket_cap_elems=MICRO_Q8_CAP))
+        inners.append(inner)
+    for s in (1, 2):
+        if n == 1:  # the engine's own single-replica path
+            e = engines[0]
+            th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+            synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in inners[0]])
+            e.step()
+            torch.cuda.synchronize()
+        else:
+            _q8_emulated_step(engines, inners, s)
+        for e, inner in zip(engines, inners):
+            th = np.concatenate(_host(e.unpacked(e.theta)))
+            assert th.tobytes() == exp[f"theta_s{s}"].tobytes(), (n, s)
+            assert np.concatenate(_host(inner)).tobytes() == th.tobytes()
+
+
+def test_int8_wire_t125_error_and_ragged_tails():
+    """Full T125 tree (tails, 148 tensors): one step through the int8 wire vs the exact fp32
+    step -- deltas quantised twice, each |err| <= s/2 with s = amax/127 per 4096-chunk."""
+    spec = get_tree("t125")
+    shapes = [s for _, s in spec.params()]
+    pa = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
+    pb = [t.clone() for t in pa]
+    ea = OuterSync(pa, world_size=1, wire_dtype=torch.int8)
+    eb = OuterSync(pb, world_size=1)
+    for e, ps in ((ea, pa), (eb, pb)):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, 1, 0, out=[p.view(-1) for p in ps])
+        e.step()
+    torch.cuda.synchronize()
+    # θ_1 = θ_0 - lr*(1+m)*g: compare the applied updates
+    th0 = synth.outer_tree_device(spec, DEV)
+    worst = 0.0
+    for a, b, t0 in zip(ea.unpacked(ea.theta), eb.unpacked(eb.theta), th0):
+        ua, ub = (t0.view(-1) - a.reshape(-1)), (t0.view(-1) - b.reshape(-1))
+        worst = max(worst, float((ua - ub).abs().max() / ub.abs().max().clamp_min(1e-30)))
+    assert worst < 1.6e-2, worst
+    ea.close()
+    eb.close()

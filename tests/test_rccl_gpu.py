@@ -123,3 +123,44 @@ def test_rccl_single_rank_transport_bit_exact():
     assert rec["t125_equal"][0]
     assert rec["bf16_equal"][0]
     assert rec["gradsync_equal"][0]
+
+
+def _worker_q8(rank, port, out):
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from datetime import timedelta
+
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                            timeout=timedelta(seconds=120))
+    from diloco_amd import synth
+    from diloco_amd.outer import OuterSync
+    from diloco_amd.trees import get_tree
+    from expect import MICRO_Q8_CAP
+
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+    eng = OuterSync(params, world_size=1, wire_dtype=torch.int8, bucket_cap_elems=MICRO_Q8_CAP)
+    rec = {}
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in eng.unpacked(eng.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        eng.step(pipeline=True)  # all_to_all + all_gather through RCCL
+        torch.cuda.synchronize()
+        rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
+    np.savez(os.path.join(out, "q8.npz"), **rec)
+    dist.destroy_process_group()
+
+
+def test_rccl_single_rank_int8_exchange():
+    from expect import expected_q8
+
+    out = tempfile.mkdtemp(prefix="dl_rccl_q8_")
+    mp.spawn(_worker_q8, args=(_free_port(), out), nprocs=1, join=True)
+    rec = dict(np.load(os.path.join(out, "q8.npz")))
+    exp = expected_q8(1)
+    for s in (1, 2):
+        assert rec[f"theta_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes()
