@@ -238,6 +238,120 @@ def parity_check(dev, ws, rank, wire):
             "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
 
 
+def run_q8(spec, dev, ws, rank, steps, warmup, cap):
+    """int8 wire: per-bucket dl_delta_q8 -> all_to_all -> dl_q8_reduce ->
+    all_gather -> dl_unpack_sgd_q8. Bus bytes per peer: 2(n-1)/n * slot bytes (1.016 B/param)
+    instead of 2(n-1)/n * 4 B/param. At one replica the exchange is skipped; the kernels run."""
+    from diloco_amd.kernels import Q8_SLOT
+
+    eng = build(spec, dev, rank, torch.int8, cap)
+    P = spec.total()
+    for _ in range(max(warmup, 1)):
+        eng.step()
+    _sync(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step()
+    _sync(ws)
+    dt = _max_over_ranks(time.perf_counter() - t0, dev, ws)
+    nb = eng.tree.n_buckets
+    slot_bytes = eng.tree.n_chunks * Q8_SLOT
+    res = {"tree": spec.name, "params": P, "buckets": nb, "chunks": eng.tree.n_chunks,
+           "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * P / (dt / steps) / 1e9,
+           "wire": "int8", "wire_bytes_per_param": round(slot_bytes / P, 4),
+           "bus_bytes_per_step": 2.0 * (ws - 1) / ws * slot_bytes}
+    if ws == 1:  # the three kernels, each over the whole tree, timed in place
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        tot = [0.0, 0.0, 0.0]
+        for _ in range(steps):
+            ev[0].record()
+            for b in range(nb):
+                eng.pseudo_gradient(b)
+            ev[1].record()
+            for b in range(nb):
+                region = eng.q8_region(b)
+                eng.k.q8_reduce(region, 1, eng.q8_plan[b][1], 1, region)
+            ev[2].record()
+            for b in range(nb):
+                eng.apply(b)
+            ev[3].record()
+            eng.steps_done += 1
+            torch.cuda.synchronize()
+            for i in range(3):
+                tot[i] += ev[i].elapsed_time(ev[i + 1])
+        ms = [t / steps for t in tot]
+        res["kernels"] = {
+            "delta_q8": kernel_entry(8 * P + slot_bytes, ms[0]),
+            "q8_reduce": kernel_entry(2 * slot_bytes, ms[1]),
+            "unpack_sgd_q8": kernel_entry(slot_bytes + 20 * P, ms[2]),
+        }
+    eng.close()
+    del eng
+    torch.cuda.empty_cache()
+    return res
+
+
+def parity_q8(dev, ws, rank):
+    """int8 codec on the tiny tree (3 buckets): the averaged g every replica applies against the
+    exact fp32 average, element by element, within the quantiser's own bound
+        |g - avg| <= (1/n) Σ_r s_r/2 + s'/2,   s_r = amax_chunk(delta_r)/127,
+        s' = amax_chunk(avg')/127 <= (amax_chunk(avg) + (1/n) Σ_r s_r/2)/127
+    (plus 1e-5 relative slack for the fp32 sums); and every replica bit-identical after it."""
+    from diloco_amd.kernels import Q8_SLOT
+
+    spec = get_tree("tiny")
+    eng = build(spec, dev, rank, torch.int8, 1 << 20)
+    nb = eng.tree.n_buckets
+    deq = []
+    for b in range(nb):
+        eng.pseudo_gradient(b)
+        nch, m, _ = eng.q8_plan[b]
+        if ws > 1:
+            eng.q8_exchange(b).wait()
+        else:
+            region = eng.q8_region(b)
+            eng.k.q8_reduce(region, 1, m, 1, region)
+        sl = eng.q8_region(b).view(-1, Q8_SLOT)[:nch]
+        scale = sl[:, :4].contiguous().view(torch.float32)
+        deq.append(sl[:, 64:].contiguous().view(torch.int8).float() * scale)
+    deq = torch.cat(deq)  # [n_chunks, 4096], tree chunk order
+    theta0 = synth.outer_tree_device(spec, dev)
+    deltas = [[t - i for t, i in zip(theta0, synth.inner_tree_device(theta0, 1, r))]
+              for r in range(ws)]
+
+    def rows(x):  # one tensor -> its chunks, zero-padded to 4096
+        k = -(-x.numel() // 4096)
+        return torch.nn.functional.pad(x.reshape(-1), (0, k * 4096 - x.numel())).view(k, 4096)
+
+    worst, c = 0.0, 0
+    for t in range(len(theta0)):
+        ref = deltas[0][t].clone()
+        for r in range(1, ws):
+            ref = ref + deltas[r][t]
+        if ws > 1:
+            ref = ref / ws
+        R = rows(ref)
+        k = R.shape[0]
+        half_s = sum(rows(deltas[r][t]).abs().amax(1, keepdim=True) / 254 for r in range(ws)) / ws
+        s2 = (R.abs().amax(1, keepdim=True) + half_s) / 127
+        bound = (half_s + s2 / 2) * (1 + 1e-5) + 1e-30
+        worst = max(worst, float(((deq[c:c + k] - R).abs() / bound).max()))
+        c += k
+    for b in range(nb):
+        eng.apply(b)
+    eng.steps_done += 1
+    torch.cuda.synchronize()
+    bits = eng.theta.view(torch.int32).to(torch.int64).sum()
+    ck = torch.stack([bits, -bits])
+    if ws > 1:
+        dist.all_reduce(ck, op=dist.ReduceOp.MAX)
+    identical = bool(ck[0].item() == -ck[1].item())
+    eng.close()
+    return {"tree": "tiny", "buckets": nb, "wire": "int8",
+            "max_err_over_bound": worst, "tolerance": 1.0,
+            "replicas_identical": identical, "ok": bool(worst <= 1.0 and identical)}
+
+
 def dropin_rate(spec, dev, ws, rank, steps):
     """The reference's call sequence (src/train.py:261-269) through the drop-in functions:
     host-resident outer model, PCIe transfers included (DESIGN.md "Host-memory ends")."""
@@ -354,7 +468,8 @@ def _guard(fn, *a, **k):
 
 
 def _brief(r):
-    keep = ("value", "ms_per_step", "roofline", "kernels", "buckets", "params", "wire")
+    keep = ("value", "ms_per_step", "roofline", "kernels", "buckets", "params", "wire",
+            "wire_bytes_per_param", "bus_bytes_per_step")
     return {k: r[k] for k in keep if k in r}
 
 
@@ -397,12 +512,15 @@ def main():
             if wire == torch.float32:  # BASELINE config #5: bf16 wire + SGD fused into unpack
                 r = _guard(run_tree, es, dev, ws, rank, ks, 1, torch.bfloat16, cap)
                 extra[f"{es.name}_bf16_wire"] = _brief(r) if "value" in r else r
+                r = _guard(run_q8, es, dev, ws, rank, ks, 1, cap)  # §8f row 4: int8 wire
+                extra[f"{es.name}_int8_wire"] = _brief(r) if "value" in r else r
         if ws > 1:
             extra[f"{spec.name}_dp_grad_sync"] = _guard(gradsync_rate, spec, dev, ws, rank,
                                                         max(3, a.steps // 2))
         if not a.no_parity:
             parity = {"f32": _guard(parity_check, dev, ws, rank, torch.float32),
-                      "bf16": _guard(parity_check, dev, ws, rank, torch.bfloat16)}
+                      "bf16": _guard(parity_check, dev, ws, rank, torch.bfloat16),
+                      "int8": _guard(parity_q8, dev, ws, rank)}
         if not a.no_dropin:
             dropin = _guard(dropin_rate, spec, dev, ws, rank, 5)
         if rank == 0 and ws == 1 and not a.no_cpu_baseline:
