@@ -70,12 +70,12 @@ def setup_dist(n_gpus):
     return ws, rank, dev
 
 
-def build(spec, dev, rank, wire, cap, fuse=False):
+def build(spec, dev, rank, wire, cap, fuse=False, shard=None):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree_device(spec, dev)
     params = [t.view(s) for t, s in zip(theta0, shapes)]
     eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=wire,
-                    bucket_cap_elems=cap, fuse_single=fuse)
+                    bucket_cap_elems=cap, fuse_single=fuse, shard=shard)
     # inner = θ_0 + this rank's noise (stands in for H inner steps)
     synth.inner_tree_device([p.view(-1) for p in params], 1, rank, out=[p.view(-1) for p in params])
     return eng
@@ -103,11 +103,12 @@ def kernel_entry(bytes_per_launch, ms, traffic=None, bound="hbm", peak=HBM_PEAK_
             "bytes_per_launch": bytes_per_launch, "avg_ms": round(ms, 5)}
 
 
-def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loops=True):
+def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loops=True,
+             shard=None):
     """Timed region (K outer steps, nothing else on the stream), then an instrumented pass of
     K more steps with HIP events between the kernels on the stream they run on (events in the
     timed region would cost the step ~35 us each), then the same kernels back to back."""
-    eng = build(spec, dev, rank, wire, cap, fuse)
+    eng = build(spec, dev, rank, wire, cap, fuse, shard)
     P = spec.total()
     for _ in range(max(warmup, 1)):  # >= 1: the timed steps run the steady-state SGD mode
         eng.step()
@@ -142,7 +143,9 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
     res = {"tree": spec.name, "params": P, "tensors": len(spec.params()),
            "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
            "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * P / (dt / steps) / 1e9,
-           "wire": "bf16" if wire == torch.bfloat16 else "f32"}
+           "wire": "bf16" if wire == torch.bfloat16 else "f32",
+           "variant": ("reduce_scatter -> shard SGD -> all_gather" if eng.sharded
+                       else "all_reduce -> replicated SGD")}
     if single and fuse:
         b = 24 * P  # read θ, inner, buf; write θ, buf, inner
         res["kernels"] = {"delta_sgd": kernel_entry(b, first, pmc.get("delta_sgd"))}
@@ -165,7 +168,7 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         e1.synchronize()
         return e0.elapsed_time(e1) / reps
 
-    if b2b_loops:
+    if b2b_loops and not eng.sharded:
         res["kernels_b2b"] = {"delta_pack": kernel_entry((8 + wb) * P, b2b(eng.pseudo_gradient)),
                               "unpack_sgd": kernel_entry((wb + 20) * P, b2b(eng.apply))}
     if single:
@@ -173,24 +176,31 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         dom = max(ks, key=lambda k: ks[k]["avg_ms"])
         res["roofline"] = dict(ks[dom], kernel=dom)
     else:
-        def allreduce_all():
+        def collectives_all():
             for b in range(eng.tree.n_buckets):
-                eng.all_reduce(b, async_op=False)
+                if eng.sharded:
+                    eng.reduce_scatter(b, async_op=False)
+                    eng.all_gather(b, async_op=False)
+                else:
+                    eng.all_reduce(b, async_op=False)
 
         reps_ar = max(3, steps // 2)
         _sync(ws)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps_ar):
-            allreduce_all()
+            collectives_all()
         e1.record()
         e1.synchronize()
         ar_ms = _max_over_ranks(e0.elapsed_time(e1) / reps_ar, dev, ws)
-        bus = 2.0 * (ws - 1) / ws * wb * eng.tree.total
+        # all-reduce: 2(n-1)/n · wire bytes; sharded: (n-1)/n · wire (RS) + (n-1)/n · 4 B (AG of θ)
+        frac = (ws - 1) / ws * eng.tree.total
+        bus = frac * (wb + 4) if eng.sharded else 2.0 * frac * wb
+        name = ("rccl reduce_scatter + all_gather (all buckets, back to back)" if eng.sharded
+                else "rccl all_reduce (all buckets, back to back)")
         res["roofline"] = dict(kernel_entry(bus, ar_ms, bound="xgmi",
                                             peak=(ws - 1) * XGMI_LINK_GBS),
-                               kernel="rccl all_reduce (all buckets, back to back)",
-                               bus_bytes_per_step=bus)
+                               kernel=name, bus_bytes_per_step=bus)
     eng.close()
     del eng
     torch.cuda.empty_cache()
@@ -203,7 +213,7 @@ def parity_check(dev, ws, rank, wire):
     tolerance). bf16 wire: the codec error vs the exact fp32 average, bound n*2^-8. Both: every
     replica bit-identical after the full step."""
     spec = get_tree("tiny")
-    eng = build(spec, dev, rank, wire, 1 << 20)
+    eng = build(spec, dev, rank, wire, 1 << 20, shard=False)
     nb = eng.tree.n_buckets
     for b in range(nb):
         eng.pseudo_gradient(b)
@@ -236,6 +246,43 @@ def parity_check(dev, ws, rank, wire):
     return {"tree": "tiny", "buckets": nb, "wire": "f32" if wire == torch.float32 else "bf16",
             "avg_delta_normwise_err": worst, "tolerance": tol,
             "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
+
+
+def parity_sharded(dev, ws, rank):
+    """The sharded step (reduce-scatter -> dl_shard_sgd -> all-gather -> dl_scatter) against
+    the replicated one (all-reduce -> dl_unpack_sgd) on the tiny tree, 2 outer steps: θ,
+    momentum and inner normwise <= 1e-6 per tensor (bit-exact where the two collectives sum in
+    the same order), every replica bit-identical."""
+    spec = get_tree("tiny")
+    ea = build(spec, dev, rank, torch.float32, 1 << 20, shard=True)
+    eb = build(spec, dev, rank, torch.float32, 1 << 20, shard=False)
+    for s in (1, 2):
+        for e in (ea, eb):
+            if s > 1:
+                th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+                synth.inner_tree_device(th, s, rank, out=[p.view(-1) for p in e.params])
+            e.step(pipeline=True)
+    torch.cuda.synchronize()
+    worst, exact = 0.0, True
+    ma, mb = ea.momentum_full(), eb.momentum_full()
+    for x, y in ((ea.theta, eb.theta), (ma, mb)):
+        exact &= bool(torch.equal(x, y))
+        for a, b in zip(ea.unpacked(x), eb.unpacked(y)):
+            scale = float(b.abs().max().clamp_min(1e-30))
+            worst = max(worst, float((a - b).abs().max()) / scale)
+    inner_ok = all(torch.equal(p, t) for p, t in zip(ea.params, ea.unpacked(ea.theta)))
+    bits = ea.theta.view(torch.int32).to(torch.int64).sum()
+    ck = torch.stack([bits, -bits])
+    if ws > 1:
+        dist.all_reduce(ck, op=dist.ReduceOp.MAX)
+    identical = bool(ck[0].item() == -ck[1].item())
+    buckets = ea.tree.n_buckets
+    ea.close()
+    eb.close()
+    return {"tree": "tiny", "buckets": buckets, "steps": 2,
+            "sharded_vs_replicated_normwise_err": worst, "bit_exact": exact,
+            "tolerance": 1e-6, "inner_is_theta": inner_ok, "replicas_identical": identical,
+            "ok": bool(worst <= 1e-6 and identical and inner_ok)}
 
 
 def run_q8(spec, dev, ws, rank, steps, warmup, cap):
@@ -468,7 +515,7 @@ def _guard(fn, *a, **k):
 
 
 def _brief(r):
-    keep = ("value", "ms_per_step", "roofline", "kernels", "buckets", "params", "wire",
+    keep = ("value", "ms_per_step", "roofline", "kernels", "buckets", "params", "wire", "variant",
             "wire_bytes_per_param", "bus_bytes_per_step")
     return {k: r[k] for k in keep if k in r}
 
@@ -515,12 +562,17 @@ def main():
                 r = _guard(run_q8, es, dev, ws, rank, ks, 1, cap)  # §8f row 4: int8 wire
                 extra[f"{es.name}_int8_wire"] = _brief(r) if "value" in r else r
         if ws > 1:
+            # the replicated variant (all-reduce -> SGD on every peer) beside the sharded headline
+            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, cap, False,
+                       False, False)
+            extra[f"{spec.name}_allreduce_variant"] = _brief(r) if "value" in r else r
             extra[f"{spec.name}_dp_grad_sync"] = _guard(gradsync_rate, spec, dev, ws, rank,
                                                         max(3, a.steps // 2))
         if not a.no_parity:
             parity = {"f32": _guard(parity_check, dev, ws, rank, torch.float32),
                       "bf16": _guard(parity_check, dev, ws, rank, torch.bfloat16),
-                      "int8": _guard(parity_q8, dev, ws, rank)}
+                      "int8": _guard(parity_q8, dev, ws, rank),
+                      "sharded": _guard(parity_sharded, dev, ws, rank)}
         if not a.no_dropin:
             dropin = _guard(dropin_rate, spec, dev, ws, rank, 5)
         if rank == 0 and ws == 1 and not a.no_cpu_baseline:
@@ -542,8 +594,9 @@ def main():
             "data": "synthetic (counter-based GPT-2-shaped tree, SURVEY.md §8d)",
             "config": {
                 "workload": (f"DiLoCo outer step, {spec.name} tree per rank: delta_pack -> "
-                             + ("RCCL all_reduce (bucketed, pipelined) -> " if ws > 1 else "")
-                             + "unpack_sgd (+copy to inner)"),
+                             + ("RCCL reduce_scatter -> shard_sgd (1/n of θ, momentum) -> RCCL "
+                                "all_gather(θ) -> scatter to inner (bucketed, pipelined)"
+                                if ws > 1 else "unpack_sgd (+copy to inner)")),
                 "tree": spec.name, "params": main_res["params"], "tensors": main_res["tensors"],
                 "wire": a.wire, "buckets": main_res["buckets"], "chunks": main_res["chunks"],
                 "parallelism": f"dp{ws}",

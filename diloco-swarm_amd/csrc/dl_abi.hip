@@ -37,21 +37,30 @@ int hip_fail(hipError_t e, const char* where) {
 int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 // The planner rule (frozen; bit-exact contract with oracle/diloco_oracle.c:or_plan_tables and
-// diloco_amd/plan.py). Returns number of buckets.
-int plan(const int64_t* numel, int32_t n, int64_t cap, int32_t align, int64_t* seg_off,
-         int64_t* bounds) {
-  seg_off[0] = 0;
-  for (int32_t i = 0; i < n; ++i) seg_off[i + 1] = align_up(seg_off[i] + numel[i], align);
+// diloco_amd/plan.py). Tensors are placed in order at align-element boundaries; a tensor that
+// would push the current bucket's padded size past cap starts a new bucket (never the first
+// tensor of a bucket), and a bucket starts at a bucket_align boundary (bucket_align == align:
+// no gap). seg_off[n] = end of the tree, rounded up to bucket_align. Returns number of buckets.
+int plan(const int64_t* numel, int32_t n, int64_t cap, int32_t align, int64_t bucket_align,
+         int64_t* seg_off, int64_t* bounds) {
+  bounds[0] = 0;
   if (n == 0) {
-    bounds[0] = 0;
+    seg_off[0] = 0;
     return 0;
   }
   int nb = 0;
-  bounds[0] = 0;
+  int64_t pos = 0, bstart = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const int64_t start = bounds[nb];
-    if (cap > 0 && i > start && seg_off[i + 1] - seg_off[start] > cap) bounds[++nb] = i;
+    int64_t s = pos, e = align_up(s + numel[i], align);
+    if (cap > 0 && i > bounds[nb] && e - bstart > cap) {
+      s = bstart = align_up(pos, bucket_align);
+      e = align_up(s + numel[i], align);
+      bounds[++nb] = i;
+    }
+    seg_off[i] = s;
+    pos = e;
   }
+  seg_off[n] = align_up(pos, bucket_align);
   bounds[++nb] = n;
   return nb;
 }
@@ -80,18 +89,33 @@ extern "C" {
 DL_API const char* dl_last_error(void) { return g_err.c_str(); }
 DL_API int dl_abi_version(void) { return DL_ABI_VERSION; }
 
-DL_API int dl_plan_tables(const int64_t* numel, int32_t n, int64_t cap_elems, int32_t align_elems,
-                          int64_t* seg_off, int64_t* bkt_bounds, int32_t* n_bkt) {
+DL_API int dl_plan_tables_ex(const int64_t* numel, int32_t n, int64_t cap_elems,
+                             int32_t align_elems, int64_t bucket_align_elems, int64_t* seg_off,
+                             int64_t* bkt_bounds, int32_t* n_bkt) {
   if (n < 0 || (n > 0 && !numel) || !seg_off || !bkt_bounds || !n_bkt)
     return fail(DL_E_ARG, "dl_plan_tables: null pointer or n < 0");
   if (align_elems <= 0) return fail(DL_E_ARG, "dl_plan_tables: align_elems must be > 0");
+  if (bucket_align_elems <= 0 || bucket_align_elems % align_elems)
+    return fail(DL_E_ARG, "dl_plan_tables: bucket_align %lld is not a positive multiple of %d",
+                (long long)bucket_align_elems, align_elems);
   for (int32_t i = 0; i < n; ++i)
     if (numel[i] < 0) return fail(DL_E_ARG, "dl_plan_tables: numel[%d] < 0", i);
-  *n_bkt = plan(numel, n, cap_elems, align_elems, seg_off, bkt_bounds);
+  *n_bkt = plan(numel, n, cap_elems, align_elems, bucket_align_elems, seg_off, bkt_bounds);
   return DL_OK;
 }
 
+DL_API int dl_plan_tables(const int64_t* numel, int32_t n, int64_t cap_elems, int32_t align_elems,
+                          int64_t* seg_off, int64_t* bkt_bounds, int32_t* n_bkt) {
+  return dl_plan_tables_ex(numel, n, cap_elems, align_elems, align_elems, seg_off, bkt_bounds,
+                           n_bkt);
+}
+
 DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl_tree_t* out) {
+  return dl_tree_create_ex(numel, n, cap_elems, DL_ALIGN_ELEMS, out);
+}
+
+DL_API int dl_tree_create_ex(const int64_t* numel, int32_t n, int64_t cap_elems,
+                             int64_t bucket_align_elems, dl_tree_t* out) {
   if (!out) return fail(DL_E_ARG, "dl_tree_create: out is null");
   *out = nullptr;
   if (n < 0 || (n > 0 && !numel)) return fail(DL_E_ARG, "dl_tree_create: bad numel/n");
@@ -102,8 +126,8 @@ DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl
   t->seg_off.resize(size_t(n) + 1);
   t->bounds.resize(size_t(n) + 1);
   int32_t nb = 0;
-  int rc = dl_plan_tables(numel, n, cap_elems, DL_ALIGN_ELEMS, t->seg_off.data(), t->bounds.data(),
-                          &nb);
+  int rc = dl_plan_tables_ex(numel, n, cap_elems, DL_ALIGN_ELEMS, bucket_align_elems,
+                             t->seg_off.data(), t->bounds.data(), &nb);
   if (rc) {
     delete t;
     return rc;
@@ -191,7 +215,7 @@ DL_API int dl_tree_bucket_range(dl_tree_t t, int32_t b, int64_t* begin, int64_t*
   }
   if (b < 0 || b >= nb) return fail(DL_E_ARG, "dl_tree_bucket_range: bucket %d of %d", b, nb);
   *begin = t->seg_off[t->bounds[b]];
-  *end = t->seg_off[t->bounds[b + 1]];
+  *end = t->seg_off[t->bounds[b + 1]];  // next bucket's start, or seg_off[n] = the tree's end
   return DL_OK;
 }
 
@@ -366,6 +390,26 @@ DL_API int dl_delta_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer
   dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
   hipError_t e = dl::launch_delta_sgd(L, inner_slot, outer, mom, a);
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_sgd");
+}
+
+DL_API int dl_shard_sgd(const void* wire, int32_t wire_dtype, int32_t divisor, float* outer,
+                        float* mom, int64_t n, float lr, float momentum, int32_t nesterov,
+                        int32_t first_step, dl_stream_t s) {
+  if (n < 0) return fail(DL_E_ARG, "dl_shard_sgd: n %lld", (long long)n);
+  if (n == 0) return DL_OK;
+  DL_TRY(check_packed(wire, "dl_shard_sgd", "wire"));
+  DL_TRY(check_dtype(wire_dtype, "dl_shard_sgd"));
+  DL_TRY(check_packed(outer, "dl_shard_sgd", "outer"));
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_shard_sgd", "momentum"));
+  if (divisor < 1) return fail(DL_E_ARG, "dl_shard_sgd: divisor %d", divisor);
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_shard_sgd: Nesterov momentum requires a momentum");
+  if ((n + DL_CHUNK_ELEMS - 1) / DL_CHUNK_ELEMS > INT32_MAX)
+    return fail(DL_E_ARG, "dl_shard_sgd: shard too large");
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_shard_sgd(wire, wire_dtype, divisor, outer, mom, n, a,
+                                      static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_shard_sgd");
 }
 
 DL_API int dl_delta_q8(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,

@@ -393,6 +393,51 @@ hipError_t launch_unpack_sgd(const Launch& L, const void* wire, int wire_dtype, 
   return unpack_sgd_t(L, static_cast<const float*>(wire), divisor, outer, mom, a, inner_slot);
 }
 
+// Sharded outer step: after the reduce-scatter each peer owns a contiguous 1/n of
+// every bucket; the same UnpackSgd body runs over it as flat 4096-element chunks (no tree, no
+// inner copy: θ is all-gathered and scattered to the inner params afterwards).
+template <class Body>
+__global__ void __launch_bounds__(kThreads) k_flat(int64_t n, Body body) {
+  for (int64_t base = int64_t(blockIdx.x) * DL_CHUNK_ELEMS; base < n;
+       base += int64_t(gridDim.x) * DL_CHUNK_ELEMS) {
+    Chunk ck;
+    ck.poff = base;
+    ck.len = int32_t(n - base < DL_CHUNK_ELEMS ? n - base : DL_CHUNK_ELEMS);
+    ck.seg = 0;
+    body.template run<true, true>(ck, 0, nullptr, 0, int(threadIdx.x));  // NT loads + stores
+  }
+}
+
+template <class Body>
+static hipError_t run_flat(int64_t n, const Body& body, hipStream_t s) {
+  const int32_t grid = int32_t((n + DL_CHUNK_ELEMS - 1) / DL_CHUNK_ELEMS);
+  hipLaunchKernelGGL(k_flat<Body>, dim3(grid), dim3(kThreads), 0, s, n, body);
+  return hipGetLastError();
+}
+
+template <typename W, bool DIV>
+static hipError_t shard_sgd_mode(const W* w, float d, float* outer, float* mom, int64_t n,
+                                 SgdArgs a, hipStream_t s) {
+  if (a.momentum == 0.f) return run_flat(n, UnpackSgd<W, DIV, 0>{w, outer, mom, d, a, -1}, s);
+  if (a.first) return run_flat(n, UnpackSgd<W, DIV, 1>{w, outer, mom, d, a, -1}, s);
+  return run_flat(n, UnpackSgd<W, DIV, 2>{w, outer, mom, d, a, -1}, s);
+}
+
+template <typename W>
+static hipError_t shard_sgd_t(const W* w, int divisor, float* outer, float* mom, int64_t n,
+                              SgdArgs a, hipStream_t s) {
+  const float d = float(divisor);
+  if (divisor == 1) return shard_sgd_mode<W, false>(w, d, outer, mom, n, a, s);
+  return shard_sgd_mode<W, true>(w, d, outer, mom, n, a, s);
+}
+
+hipError_t launch_shard_sgd(const void* wire, int wire_dtype, int divisor, float* outer, float* mom,
+                            int64_t n, SgdArgs a, hipStream_t s) {
+  if (wire_dtype == DL_BF16)
+    return shard_sgd_t(static_cast<const bf16_t*>(wire), divisor, outer, mom, n, a, s);
+  return shard_sgd_t(static_cast<const float*>(wire), divisor, outer, mom, n, a, s);
+}
+
 hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float* mom, SgdArgs a) {
   if (a.momentum == 0.f) return run(L, DeltaSgd<0>{outer, mom, a, inner_slot});
   if (a.first) return run(L, DeltaSgd<1>{outer, mom, a, inner_slot});

@@ -18,7 +18,6 @@ namespace dl {
 namespace {
 
 constexpr int kQ8Header = DL_Q8_SLOT_BYTES - DL_CHUNK_ELEMS;  // 64 B: fp32 scale + padding
-constexpr int kVals = kUnroll * 4;                           // values per lane per chunk (16)
 
 __device__ __forceinline__ float block_amax(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));  // 64-lane wave

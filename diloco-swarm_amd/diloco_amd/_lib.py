@@ -34,7 +34,9 @@ _pu64 = ctypes.POINTER(ctypes.c_uint64)
 # name -> (restype, argtypes); must list every DL_API function of include/diloco_hip.h
 SIGNATURES = {
     "dl_plan_tables": (ctypes.c_int, [_pi64, _i32, _i64, _i32, _pi64, _pi64, _pi32]),
+    "dl_plan_tables_ex": (ctypes.c_int, [_pi64, _i32, _i64, _i32, _i64, _pi64, _pi64, _pi32]),
     "dl_tree_create": (ctypes.c_int, [_pi64, _i32, _i64, ctypes.POINTER(_vp)]),
+    "dl_tree_create_ex": (ctypes.c_int, [_pi64, _i32, _i64, _i64, ctypes.POINTER(_vp)]),
     "dl_tree_destroy": (ctypes.c_int, [_vp]),
     "dl_tree_query": (ctypes.c_int, [_vp, _pi64, _pi32, _pi32, _pi32]),
     "dl_tree_bucket_range": (ctypes.c_int, [_vp, _i32, _pi64, _pi64]),
@@ -49,6 +51,9 @@ SIGNATURES = {
         [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _i32, _vp],
     ),
     "dl_delta_sgd": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _vp]),
+    "dl_shard_sgd": (
+        ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _vp],
+    ),
     "dl_delta_q8": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
     "dl_q8_reduce": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _vp]),
     "dl_unpack_sgd_q8": (

@@ -46,10 +46,11 @@ class HipKernels:
         _lib.load()
 
     def tree(self, numels: Sequence[int], device: torch.device,
-             cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS) -> PackedTree:
+             cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS,
+             bucket_align: int = _lib.ALIGN_ELEMS) -> PackedTree:
         self.check_device(device)
         with torch.cuda.device(device):
-            return PackedTree(numels, cap_elems)
+            return PackedTree(numels, cap_elems, bucket_align)
 
     def bind(self, tree: PackedTree, slot: int, tensors: Sequence[torch.Tensor], device) -> None:
         tree.bind(slot, tensors, torch.cuda.current_stream(device).cuda_stream)
@@ -68,6 +69,12 @@ class HipKernels:
                   first) -> None:
         _lib.call("dl_delta_sgd", tree.handle, bucket, inner_slot, theta.data_ptr(), _ptr(mom),
                   float(lr), float(momentum), int(nesterov), int(first), _s(theta))
+
+    def shard_sgd(self, wire, divisor, theta, mom, lr, momentum, nesterov, first) -> None:
+        """Flat 1/n shard after a reduce-scatter (wire, theta, mom: equal-length views)."""
+        _lib.call("dl_shard_sgd", wire.data_ptr(), wire_code(wire.dtype), int(divisor),
+                  theta.data_ptr(), _ptr(mom), theta.numel(), float(lr), float(momentum),
+                  int(nesterov), int(first), _s(theta))
 
     # int8 wire codec (DL_Q8_SLOT_BYTES slots, one per chunk)
     def delta_q8(self, tree, bucket, inner_slot, theta, slots) -> None:

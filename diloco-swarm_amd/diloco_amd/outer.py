@@ -8,6 +8,11 @@ One `OuterSync` per DP replica (one process per GPU). It performs, for the whole
     outer_optimizer.step()    (src/train.py:267)      -> dl_unpack_sgd   g = wire/n; Nesterov SGD
     sync_inner_model          (src/utils.py:223-226)  -> (fused in dl_unpack_sgd) inner = θ
 
+With n > 1 replicas the default is the sharded variant of SURVEY §8e (shard=True): per bucket
+reduce-scatter of the wire -> dl_shard_sgd on this peer's 1/n (θ and momentum shards, ZeRO-1
+style) -> all-gather of θ -> dl_scatter into the inner params. Same bus bytes as the
+all-reduce; HBM traffic per peer 20 + 20/n B/param instead of 36, momentum memory 4P/n.
+
 With one replica (no all-reduce, src/comm.py:118-119) the default is a single pass,
 dl_delta_sgd: the delta stays in registers (24 instead of 36 B/param); fuse_single=False
 keeps the two-kernel pipeline (BASELINE config #2's delta+pack -> unpack).
@@ -52,6 +57,13 @@ def pipelined_buckets(n_buckets: int, pack: Callable[[int], None],
         unpack(n_buckets - 1)
 
 
+class _Done:
+    """Handle of a collective that completed synchronously (one replica, no process group)."""
+
+    def wait(self) -> None:
+        pass
+
+
 class OuterSync:
     """Device-resident outer state of one replica + the fused outer step."""
 
@@ -69,6 +81,8 @@ class OuterSync:
         kernels=None,
         fuse_single: bool = True,
         side_stream: bool = True,
+        shard: Optional[bool] = None,
+        rank: Optional[int] = None,
     ):
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
                                            for p in params]
@@ -86,17 +100,28 @@ class OuterSync:
         if world_size is None:
             world_size = dist.get_world_size(group) if dist.is_initialized() else 1
         self.world_size = int(world_size)
-        self.tree = self.k.tree([p.numel() for p in self.params], self.device, bucket_cap_elems)
+        if rank is None:  # this peer's index in the DP group (which shard it owns)
+            rank = dist.get_rank(group) if dist.is_initialized() and self.world_size > 1 else 0
+        self.rank = int(rank)
+        if wire_dtype not in (torch.float32, torch.bfloat16, torch.int8):
+            raise ValueError(f"wire dtype {wire_dtype}: float32, bfloat16 or int8")
+        self.q8 = wire_dtype == torch.int8
+        if shard is None:
+            shard = self.world_size > 1 and not self.q8
+        if shard and self.q8:
+            raise ValueError("the int8 wire has its own exchange; shard=True needs f32/bf16")
+        self.sharded = bool(shard)
+        # sharded: every bucket starts at a multiple of 64·n elements -> n equal aligned shards
+        balign = _lib.ALIGN_ELEMS * (self.world_size if self.sharded else 1)
+        self.tree = self.k.tree([p.numel() for p in self.params], self.device, bucket_cap_elems,
+                                balign)
         self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
         # a1 get_outer_model (src/utils.py:213-216): θ_outer starts as a copy of inner.
         # zeros, so the alignment padding of every packed buffer stays zero forever.
         z = dict(device=self.device)
         self.theta = torch.zeros(self.tree.total, dtype=torch.float32, **z)
         self.mom = (torch.zeros(self.tree.total, dtype=torch.float32, **z)
-                    if self.momentum != 0 else None)
-        if wire_dtype not in (torch.float32, torch.bfloat16, torch.int8):
-            raise ValueError(f"wire dtype {wire_dtype}: float32, bfloat16 or int8")
-        self.q8 = wire_dtype == torch.int8
+                    if self.momentum != 0 and not self.sharded else None)
         if self.q8:
             # int8 codec: one Q8_SLOT-byte slot per chunk; bucket b's slots padded to a
             # multiple of the peer count so both exchanges split evenly (dl_q8.hip)
@@ -114,6 +139,22 @@ class OuterSync:
         else:
             self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, **z)
         self.k.gather(self.tree, ALL, SLOT_INNER, self.theta)
+        if self.sharded:
+            # shard b of this peer: θ[lo + r·s, lo + (r+1)·s) with s = (hi - lo)/n, kept in
+            # contiguous shard buffers at offset shard_off[b]
+            n, r = self.world_size, self.rank
+            self.shard_off, off = [], 0
+            for lo, hi in self.tree.bucket_ranges:
+                assert (hi - lo) % n == 0
+                self.shard_off.append(off)
+                off += (hi - lo) // n
+            self.shard_total = off
+            self.th_shard = torch.empty(off, dtype=torch.float32, **z)
+            for b in range(self.tree.n_buckets):
+                self.th_shard_view(b).copy_(self.theta_shard_of(b))
+            self.g_shard = torch.zeros(off, dtype=wire_dtype, **z)
+            self.mom_shard = (torch.zeros(off, dtype=torch.float32, **z)
+                              if self.momentum != 0 else None)
         self.steps_done = 0
         # step() runs on its own stream, ordered after the caller's current stream and joined
         # back into it: work other threads put on the default stream meanwhile (the
@@ -151,6 +192,73 @@ class OuterSync:
         red = self.q_red[:m * Q8_SLOT]
         self.k.q8_reduce(recv, n, m, n, red)
         return dist.all_gather_into_tensor(region, red, group=self.group, async_op=True)
+
+    # ---- sharded variant --------------------------------------------------------
+    def _shard_len(self, bucket: int) -> int:
+        lo, hi = self.tree.bucket_ranges[bucket]
+        return (hi - lo) // self.world_size
+
+    def theta_shard_of(self, bucket: int) -> torch.Tensor:
+        """This peer's slice of the full packed θ in one bucket."""
+        lo, _ = self.tree.bucket_ranges[bucket]
+        s = self._shard_len(bucket)
+        return self.theta[lo + self.rank * s:lo + (self.rank + 1) * s]
+
+    def _shard(self, buf: Optional[torch.Tensor], bucket: int) -> Optional[torch.Tensor]:
+        if buf is None:
+            return None
+        o = self.shard_off[bucket]
+        return buf[o:o + self._shard_len(bucket)]
+
+    def th_shard_view(self, bucket: int) -> torch.Tensor:
+        return self._shard(self.th_shard, bucket)
+
+    def _local(self) -> bool:
+        # one replica and no process group: both collectives are identities (plain copies)
+        return self.world_size == 1 and not dist.is_initialized()
+
+    def reduce_scatter(self, bucket: int, async_op: bool = True):
+        """SUM reduce-scatter of one wire bucket: this peer receives the sum of its 1/n."""
+        if self._local():
+            self._shard(self.g_shard, bucket).copy_(self.bucket_view(bucket))
+            return _Done()
+        return dist.reduce_scatter_tensor(self._shard(self.g_shard, bucket),
+                                          self.bucket_view(bucket), op=dist.ReduceOp.SUM,
+                                          group=self.group, async_op=async_op)
+
+    def shard_apply(self, bucket: int) -> None:
+        """g = Σ/n; Nesterov SGD on this peer's θ and momentum shards (a3 /n, a4)."""
+        self.k.shard_sgd(self._shard(self.g_shard, bucket), self.world_size,
+                         self.th_shard_view(bucket), self._shard(self.mom_shard, bucket),
+                         self.lr, self.momentum, self.nesterov, self.steps_done == 0)
+
+    def all_gather(self, bucket: int, async_op: bool = True):
+        """Every peer's updated θ shard -> the full packed θ of the bucket."""
+        lo, hi = self.tree.bucket_ranges[bucket]
+        if self._local():
+            self.theta[lo:hi].copy_(self.th_shard_view(bucket))
+            return _Done()
+        return dist.all_gather_into_tensor(self.theta[lo:hi], self.th_shard_view(bucket),
+                                           group=self.group, async_op=async_op)
+
+    def write_inner(self, bucket: int) -> None:
+        """a5: inner = θ_outer for one bucket (dl_scatter)."""
+        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+        self.k.scatter(self.tree, bucket, self.theta, SLOT_INNER)
+
+    def momentum_full(self) -> Optional[torch.Tensor]:
+        """The packed momentum of the whole tree (sharded: all-gathered; for checks/export)."""
+        if not self.sharded or self.mom_shard is None:
+            return self.mom
+        out = torch.zeros(self.tree.total, dtype=torch.float32, device=self.device)
+        for b in range(self.tree.n_buckets):
+            lo, hi = self.tree.bucket_ranges[b]
+            if self._local():
+                out[lo:hi].copy_(self._shard(self.mom_shard, b))
+            else:
+                dist.all_gather_into_tensor(out[lo:hi], self._shard(self.mom_shard, b),
+                                            group=self.group)
+        return out
 
     def bucket_view(self, bucket: int) -> torch.Tensor:
         if bucket == ALL:
@@ -194,6 +302,8 @@ class OuterSync:
             pipeline = self.world_size > 1
         if self.q8:
             self._step_q8(pipeline)
+        elif self.sharded:
+            self._step_sharded()
         elif pipeline:
             pipelined_buckets(self.tree.n_buckets, self.pseudo_gradient,
                               lambda b: self.all_reduce(b, async_op=True), self.apply)
@@ -206,6 +316,27 @@ class OuterSync:
             self.pseudo_gradient(ALL)
             self.apply(ALL)
         self.steps_done += 1
+
+    def _step_sharded(self) -> None:
+        """pack(b) -> RS(b) | shard SGD(b) -> AG(b) | scatter(b), overlapped across buckets:
+        the collective stream runs RS(0) RS(1) AG(0) RS(2) AG(1) ... while the compute stream
+        packs ahead, steps the shard in between and writes the inner params behind."""
+        nb = self.tree.n_buckets
+        rs, ag = [None] * nb, [None] * nb
+        self.pseudo_gradient(0)
+        rs[0] = self.reduce_scatter(0)
+        for b in range(nb):
+            if b + 1 < nb:
+                self.pseudo_gradient(b + 1)
+                rs[b + 1] = self.reduce_scatter(b + 1)
+            rs[b].wait()
+            self.shard_apply(b)
+            ag[b] = self.all_gather(b)
+            if b >= 1:
+                ag[b - 1].wait()
+                self.write_inner(b - 1)
+        ag[nb - 1].wait()
+        self.write_inner(nb - 1)
 
     def _step_q8(self, pipeline: bool) -> None:
         nb = self.tree.n_buckets

@@ -24,8 +24,11 @@ DEFAULT_BUCKET_CAP_ELEMS = 64 << 20  # 256 MiB of fp32 per bucket
 
 
 def plan_tables(numels: Sequence[int], cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS,
-                align_elems: int = _lib.ALIGN_ELEMS) -> Tuple[np.ndarray, np.ndarray]:
-    """(seg_off[n+1], bkt_bounds[n_bkt+1]) from the C planner (host only, no GPU needed)."""
+                align_elems: int = _lib.ALIGN_ELEMS,
+                bucket_align_elems: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """(seg_off[n+1], bkt_bounds[n_bkt+1]) from the C planner (host only, no GPU needed).
+    bucket_align_elems (0 = align_elems): every bucket starts at a multiple of it, so a bucket
+    splits into equal aligned shards for a reduce-scatter (ALIGN_ELEMS * peers)."""
     n = len(numels)
     num = np.ascontiguousarray(np.asarray(numels, dtype=np.int64))
     seg = np.zeros(n + 1, dtype=np.int64)
@@ -33,8 +36,9 @@ def plan_tables(numels: Sequence[int], cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS
     nb = ctypes.c_int32(0)
     p64 = ctypes.POINTER(ctypes.c_int64)
     _lib.call(
-        "dl_plan_tables",
+        "dl_plan_tables_ex",
         num.ctypes.data_as(p64) if n else None, n, int(cap_elems), int(align_elems),
+        int(bucket_align_elems or align_elems),
         seg.ctypes.data_as(p64), bnd.ctypes.data_as(p64), ctypes.byref(nb),
     )
     return seg, bnd[: nb.value + 1].copy()
@@ -43,15 +47,17 @@ def plan_tables(numels: Sequence[int], cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS
 class PackedTree:
     """Device handle (dl_tree_t) for one parameter tree on the current HIP device."""
 
-    def __init__(self, numels: Sequence[int], cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS):
+    def __init__(self, numels: Sequence[int], cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS,
+                 bucket_align_elems: int = _lib.ALIGN_ELEMS):
         self.numels = [int(n) for n in numels]
+        self.bucket_align = int(bucket_align_elems)
         n = len(self.numels)
         num = np.asarray(self.numels, dtype=np.int64)
         h = ctypes.c_void_p()
         _lib.call(
-            "dl_tree_create",
+            "dl_tree_create_ex",
             num.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) if n else None, n,
-            int(cap_elems), ctypes.byref(h),
+            int(cap_elems), self.bucket_align, ctypes.byref(h),
         )
         self._h = h
         tot, ns, nb, nc = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()

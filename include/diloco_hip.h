@@ -61,12 +61,23 @@ typedef void* dl_stream_t; /* hipStream_t */
  * oracle/diloco_oracle.c:or_plan_tables. */
 DL_API int dl_plan_tables(const int64_t* numel, int32_t n, int64_t cap_elems, int32_t align_elems,
                           int64_t* seg_off, int64_t* bkt_bounds, int32_t* n_bkt);
+/* Same rule with every bucket starting at a multiple of bucket_align_elems (a positive
+ * multiple of align_elems) and seg_off[n] rounded up to it, so each bucket's range
+ * [seg_off[bkt_bounds[b]], seg_off[bkt_bounds[b+1]]) splits into equal, aligned shards for a
+ * reduce-scatter over n peers (bucket_align = DL_ALIGN_ELEMS * n). bucket_align ==
+ * align_elems is dl_plan_tables. */
+DL_API int dl_plan_tables_ex(const int64_t* numel, int32_t n, int64_t cap_elems,
+                             int32_t align_elems, int64_t bucket_align_elems, int64_t* seg_off,
+                             int64_t* bkt_bounds, int32_t* n_bkt);
 
 /* ---- tree handle ------------------------------------------------------------------------
  * One parameter tree on the current device: planner tables + the chunk table + DL_MAX_SLOTS
  * per-tensor device pointer tables. Created once per model (src/utils.py:213-216
  * get_outer_model / src/comm.py:81 TrainingComm.__init__ are the natural creation points). */
 DL_API int dl_tree_create(const int64_t* numel, int32_t n, int64_t cap_elems, dl_tree_t* out);
+/* dl_tree_create with the dl_plan_tables_ex bucket alignment (the sharded outer step). */
+DL_API int dl_tree_create_ex(const int64_t* numel, int32_t n, int64_t cap_elems,
+                             int64_t bucket_align_elems, dl_tree_t* out);
 DL_API int dl_tree_destroy(dl_tree_t tree);
 DL_API int dl_tree_query(dl_tree_t tree, int64_t* total_elems, int32_t* n_seg, int32_t* n_bkt,
                          int32_t* n_chunk);
@@ -136,6 +147,15 @@ DL_API int dl_gather(dl_tree_t tree, int32_t bucket, int32_t src_slot, void* pac
 /* a5: sync_inner_model, src/utils.py:223-226: dst[seg][j] = packed[k] (fp32). */
 DL_API int dl_scatter(dl_tree_t tree, int32_t bucket, const float* packed, int32_t dst_slot,
                       dl_stream_t stream);
+
+/* a3 /n + a4 on one peer's shard after a reduce-scatter (the sharded variant):
+ * flat contiguous arrays of n elements, no tree: g = wire[k] / divisor (divisor 1: untouched),
+ * SGD exactly as dl_unpack_sgd on outer[k], mom[k]. The caller all-gathers `outer` and
+ * scatters it to the inner params (dl_scatter) afterwards. 20 B/param of the shard. All
+ * pointers 16-B aligned. */
+DL_API int dl_shard_sgd(const void* wire, int32_t wire_dtype, int32_t divisor, float* outer,
+                        float* mom, int64_t n, float lr, float momentum, int32_t nesterov,
+                        int32_t first_step, dl_stream_t stream);
 
 /* ---- int8 wire codec (not in the reference) --------------------------
  * One DL_Q8_SLOT_BYTES slot per chunk of the bucket, in chunk order: fp32 scale at byte 0,

@@ -17,8 +17,8 @@
  *                   param.add_(u, alpha=-lr)   -> fmaf(u, -lr, θ)
  *                 momentum == 0: θ = fmaf(g, -lr, θ) (no buffer)
  *   or_copy       src/utils.py:223-226   inner = outer
- *   or_plan_tables  the build's packed layout (no reference counterpart: the reference walks
- *                 model.parameters() in order, src/comm.py:120); rule frozen in DESIGN.md.
+ *   or_plan_tables(_ex)  the build's packed layout (no reference counterpart: the reference
+ *                 walks model.parameters() in order, src/comm.py:120); rule frozen in DESIGN.md.
  * Build: make -C oracle  (gcc, -O2 -ffp-contract=off so only the fmaf calls fuse).
  */
 #include <math.h>
@@ -27,29 +27,44 @@
 
 #define OR_API __attribute__((visibility("default")))
 
-OR_API int or_plan_tables(const int64_t* numel, int32_t n, int64_t cap, int32_t align,
-                          int64_t* seg_off, int64_t* bounds, int32_t* n_bkt) {
-  if (n < 0 || align <= 0) return -1;
-  seg_off[0] = 0;
-  for (int32_t i = 0; i < n; ++i) {
-    if (numel[i] < 0) return -1;
-    int64_t end = seg_off[i] + numel[i];
-    seg_off[i + 1] = (end + align - 1) / align * align;
-  }
+/* Placement rule restated from DESIGN.md §2: tensor i goes at the next align boundary; if
+ * that pushes the current bucket's padded size past cap (and i is not the bucket's first
+ * tensor) i opens a new bucket, which starts at the next bucket_align boundary. */
+OR_API int or_plan_tables_ex(const int64_t* numel, int32_t n, int64_t cap, int32_t align,
+                             int64_t bucket_align, int64_t* seg_off, int64_t* bounds,
+                             int32_t* n_bkt) {
+  if (n < 0 || align <= 0 || bucket_align <= 0 || bucket_align % align) return -1;
+  bounds[0] = 0;
   if (n == 0) {
-    bounds[0] = 0;
+    seg_off[0] = 0;
     *n_bkt = 0;
     return 0;
   }
   int32_t nb = 0;
-  bounds[0] = 0;
+  int64_t next = 0, bucket_begin = 0;
   for (int32_t i = 0; i < n; ++i) {
-    int64_t start = bounds[nb];
-    if (cap > 0 && i > start && seg_off[i + 1] - seg_off[start] > cap) bounds[++nb] = i;
+    if (numel[i] < 0) return -1;
+    int64_t at = next;
+    int64_t end = (at + numel[i] + align - 1) / align * align;
+    if (cap > 0 && i > bounds[nb] && end - bucket_begin > cap) {
+      at = (next + bucket_align - 1) / bucket_align * bucket_align;
+      bucket_begin = at;
+      end = (at + numel[i] + align - 1) / align * align;
+      bounds[++nb] = i;
+    }
+    seg_off[i] = at;
+    next = end;
   }
+  seg_off[n] = (next + bucket_align - 1) / bucket_align * bucket_align;
   bounds[++nb] = n;
   *n_bkt = nb;
   return 0;
+}
+
+OR_API int or_plan_tables(const int64_t* numel, int32_t n, int64_t cap, int32_t align,
+                          int64_t* seg_off, int64_t* bounds, int32_t* n_bkt) {
+  if (align <= 0) return -1;
+  return or_plan_tables_ex(numel, n, cap, align, align, seg_off, bounds, n_bkt);
 }
 
 OR_API void or_delta(const float* outer, const float* inner, float* out, int64_t n) {

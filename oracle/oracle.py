@@ -41,6 +41,10 @@ def load():
         lib.or_plan_tables.argtypes = [_I64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _I64,
                                        _I64, ctypes.POINTER(ctypes.c_int32)]
         lib.or_plan_tables.restype = ctypes.c_int
+        lib.or_plan_tables_ex.argtypes = [_I64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                          ctypes.c_int64, _I64, _I64,
+                                          ctypes.POINTER(ctypes.c_int32)]
+        lib.or_plan_tables_ex.restype = ctypes.c_int
         lib.or_delta.argtypes = [_F, _F, _F, ctypes.c_int64]
         lib.or_sum_avg.argtypes = [ctypes.POINTER(_F), ctypes.c_int32, _F, ctypes.c_int64]
         lib.or_sgd.argtypes = [_F, _F, _F, ctypes.c_int64, ctypes.c_float, ctypes.c_float,
@@ -66,31 +70,37 @@ def _fp(a: np.ndarray):
 
 
 # ---- planner ------------------------------------------------------------------------------
-def plan_tables(numels: Sequence[int], cap: int, align: int = 64) -> Tuple[np.ndarray, np.ndarray]:
+def plan_tables(numels: Sequence[int], cap: int, align: int = 64,
+                bucket_align: int = 0) -> Tuple[np.ndarray, np.ndarray]:
     lib = load()
     n = len(numels)
     num = np.asarray(numels, dtype=np.int64)
     seg = np.zeros(n + 1, dtype=np.int64)
     bnd = np.zeros(n + 1, dtype=np.int64)
     nb = ctypes.c_int32()
-    rc = lib.or_plan_tables(num.ctypes.data_as(_I64), n, cap, align, seg.ctypes.data_as(_I64),
-                            bnd.ctypes.data_as(_I64), ctypes.byref(nb))
+    rc = lib.or_plan_tables_ex(num.ctypes.data_as(_I64), n, cap, align, bucket_align or align,
+                               seg.ctypes.data_as(_I64), bnd.ctypes.data_as(_I64),
+                               ctypes.byref(nb))
     if rc:
         raise ValueError("or_plan_tables: bad arguments")
     return seg, bnd[: nb.value + 1].copy()
 
 
-def plan_tables_py(numels: Sequence[int], cap: int, align: int = 64):
+def plan_tables_py(numels: Sequence[int], cap: int, align: int = 64, bucket_align: int = 0):
     """Pure-Python statement of the same rule (cross-checks the C oracle)."""
-    seg = [0]
-    for n in numels:
-        seg.append(-(-(seg[-1] + n) // align) * align)
+    ba = bucket_align or align
+    up = lambda x, a: -(-x // a) * a  # noqa: E731
     if not numels:
-        return seg, [0]
-    bounds = [0]
-    for i in range(len(numels)):
-        if cap > 0 and i > bounds[-1] and seg[i + 1] - seg[bounds[-1]] > cap:
+        return [0], [0]
+    seg, bounds, nxt, begin = [], [0], 0, 0
+    for i, n in enumerate(numels):
+        at = nxt
+        if cap > 0 and i > bounds[-1] and up(at + n, align) - begin > cap:
+            at = begin = up(nxt, ba)
             bounds.append(i)
+        seg.append(at)
+        nxt = up(at + n, align)
+    seg.append(up(nxt, ba))
     bounds.append(len(numels))
     return seg, bounds
 

@@ -14,9 +14,10 @@ from oracle import oracle
 
 
 class CpuTree:
-    def __init__(self, numels, cap):
+    def __init__(self, numels, cap, bucket_align=64):
         self.numels = [int(n) for n in numels]
-        seg, bnd = plan_tables(self.numels, cap)
+        self.bucket_align = bucket_align
+        seg, bnd = plan_tables(self.numels, cap, bucket_align_elems=bucket_align)
         self.seg_off = seg
         self.bounds = bnd
         self.total = int(seg[-1])
@@ -54,8 +55,8 @@ class OracleKernels:
     def check_device(self, device):
         assert device.type == "cpu"
 
-    def tree(self, numels, device, cap_elems=64 << 20):
-        return CpuTree(numels, cap_elems)
+    def tree(self, numels, device, cap_elems=64 << 20, bucket_align=64):
+        return CpuTree(numels, cap_elems, bucket_align)
 
     def bind(self, tree, slot, tensors, device):
         tree.slots[slot] = [t.detach().reshape(-1) for t in tensors]
@@ -97,6 +98,17 @@ class OracleKernels:
             if mom is not None:
                 self._seg(tree, mom, i)[:] = b
             inner[:] = th
+
+    def shard_sgd(self, wire, divisor, theta, mom, lr, momentum, nesterov, first):
+        g = _np(wire).astype(np.float32)
+        if divisor != 1:
+            g = (g / np.float32(divisor)).astype(np.float32)
+        th = _np(theta).copy()
+        b = _np(mom).copy() if mom is not None else None
+        oracle.sgd(th, b, np.ascontiguousarray(g), lr, momentum, nesterov, first)
+        _np(theta)[:] = th
+        if mom is not None:
+            _np(mom)[:] = b
 
     def _chunk_range(self, tree, bucket):
         return (0, len(tree.chunks)) if bucket == -1 else tree.bucket_chunks[bucket]

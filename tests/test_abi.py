@@ -108,3 +108,38 @@ def test_planner_fuzz_against_oracle_rule():
         assert bnd.tolist() == obnd.tolist() == list(pbnd)
 
     check()
+
+
+def test_bucket_aligned_planner_fuzz_and_properties():
+    """dl_plan_tables_ex (the sharded step's layout): C planner == oracle C == Python rule; every
+    bucket starts at a multiple of bucket_align so it splits into n equal aligned shards; tensors
+    never overlap; bucket_align == align reproduces dl_plan_tables exactly."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from oracle import oracle
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.lists(st.integers(0, 300_000), max_size=60), st.integers(-1, 400_000),
+           st.sampled_from([1, 2, 3, 4, 7, 8]))
+    def check(numels, cap, peers):
+        ba = 64 * peers
+        seg, bnd = plan_tables(numels, cap, 64, ba)
+        oseg, obnd = oracle.plan_tables(numels, cap, 64, ba)
+        pseg, pbnd = oracle.plan_tables_py(numels, cap, 64, ba)
+        assert seg.tolist() == oseg.tolist() == list(pseg)
+        assert bnd.tolist() == obnd.tolist() == list(pbnd)
+        n = len(numels)
+        for i in range(n):
+            assert seg[i] % 64 == 0 and seg[i] + numels[i] <= seg[i + 1]
+        assert seg[n] % ba == 0
+        for b in range(len(bnd) - 1):
+            lo, hi = seg[bnd[b]], seg[bnd[b + 1]]
+            assert lo % ba == 0 and (hi - lo) % ba == 0
+        s1, b1 = plan_tables(numels, cap, 64, 64)
+        s0, b0 = plan_tables(numels, cap, 64)
+        assert s1.tolist() == s0.tolist() and b1.tolist() == b0.tolist()
+
+    check()
+    with pytest.raises(_lib.DilocoHipError):
+        plan_tables([1, 2], 0, 64, 96)  # not a multiple of align

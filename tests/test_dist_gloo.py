@@ -91,11 +91,14 @@ def _worker(rank, world, port, mode, num_stages, out):
                                                for p in outer.parameters()])
             sync_inner_model(outer, inner)
             rec[f"inner_s{s}"] = np.concatenate([p.detach().numpy().reshape(-1) for p in inner.parameters()])
-    elif mode == "engine":
+    elif mode in ("engine", "engine_ar"):
+        # engine: the default at n > 1, reduce-scatter -> shard SGD -> all-gather;
+        # engine_ar: the replicated variant, all-reduce -> full SGD on every peer
         params = [torch.from_numpy(v.copy()) for v in theta0]
         eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True,
                         group=world_.curr_stage_group, world_size=len(world_.dp_ranks),
-                        bucket_cap_elems=4096)
+                        bucket_cap_elems=4096, shard=None if mode == "engine" else False)
+        assert eng.sharded == (mode == "engine")
         assert eng.tree.n_buckets > 2
         for s in range(1, MICRO_STEPS + 1):
             th = eng.unpacked(eng.theta)
@@ -104,7 +107,8 @@ def _worker(rank, world, port, mode, num_stages, out):
                 p.copy_(torch.from_numpy(v))
             eng.step()
             rec[f"theta_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(eng.theta)])
-            rec[f"buf_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(eng.mom)])
+            mom = eng.momentum_full()
+            rec[f"buf_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(mom)])
             rec[f"inner_s{s}"] = np.concatenate([p.numpy().reshape(-1) for p in params])
     elif mode == "engine_q8":
         params = [torch.from_numpy(v.copy()) for v in theta0]
@@ -152,7 +156,7 @@ def _run(mode, world, num_stages=1):
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "engine"])
+@pytest.mark.parametrize("mode", ["dropin", "engine", "engine_ar"])
 def test_two_peers_match_reference_bit_exact(mode):
     g = load_npz("micro_n2.npz")
     recs = _run(mode, 2)
@@ -168,7 +172,7 @@ def test_two_peers_match_reference_bit_exact(mode):
         assert recs[1]["delta_s1"].tobytes() == g["delta_s1_rlast"].tobytes()
 
 
-@pytest.mark.parametrize("mode", ["dropin", "engine"])
+@pytest.mark.parametrize("mode", ["dropin", "engine", "engine_ar"])
 def test_four_peers_match_reference_normwise(mode):
     from diloco_amd.trees import get_tree
 

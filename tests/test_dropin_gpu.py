@@ -161,7 +161,7 @@ def _worker(rank, world, port, mode, out):
     rec = {}
     if mode == "dropin":
         rec = _outer_steps(rank, world)
-    elif mode == "engine":
+    elif mode in ("engine", "engine_ar"):
         from diloco_amd import synth
         from diloco_amd.outer import OuterSync
         from diloco_amd.trees import get_tree
@@ -169,14 +169,18 @@ def _worker(rank, world, port, mode, out):
         spec = get_tree("micro")
         shapes = [s for _, s in spec.params()]
         params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
-        eng = OuterSync(params, world_size=world, bucket_cap_elems=4096)
+        # engine: reduce-scatter -> shard SGD -> all-gather (the n > 1 default); engine_ar:
+        # all-reduce -> full SGD on each replica
+        eng = OuterSync(params, world_size=world, bucket_cap_elems=4096,
+                        shard=None if mode == "engine" else False)
+        assert eng.sharded == (mode == "engine")
         for s in (1, 2):
             th = [t.reshape(-1) for t in eng.unpacked(eng.theta)]
             synth.inner_tree_device(th, s, rank, out=[p.view(-1) for p in params])
             eng.step()
             torch.cuda.synchronize()
             rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
-            rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.mom))
+            rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.momentum_full()))
             rec[f"inner_s{s}"] = _flat(params)
     elif mode == "dp":
         from diloco_amd.comm import TrainingComm
@@ -209,7 +213,7 @@ def _run(mode, world=2):
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "engine"])
+@pytest.mark.parametrize("mode", ["dropin", "engine", "engine_ar"])
 def test_two_peers_on_gpu_match_reference(mode):
     g = load_npz("micro_n2.npz")
     for rec in _run(mode):

@@ -38,6 +38,7 @@ def _engines(spec, n, wire=torch.float32, cap=None, **kw):
     for _ in range(n):
         inner = [t.clone().view(s) for t, s in zip(theta0, shapes)]
         extra = {} if cap is None else {"bucket_cap_elems": cap}
+        kw.setdefault("shard", False)  # the emulated all-reduce drives the replicated variant
         engines.append(OuterSync(inner, world_size=n, wire_dtype=wire, **extra, **kw))
         inners.append(inner)
     return engines, inners
@@ -408,3 +409,130 @@ def test_int8_wire_t125_error_and_ragged_tails():
     assert worst < 1.6e-2, worst
     ea.close()
     eb.close()
+
+
+@pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("divisor", [1, 2, 3, 8])
+@pytest.mark.parametrize("momentum,nesterov", [(0.9, True), (0.9, False), (0.0, False)])
+def test_shard_sgd_matches_oracle(wire, divisor, momentum, nesterov):
+    """dl_shard_sgd (the sharded step's a3 /n + a4 on a flat shard) == the oracle's division and
+    SGD, bit-exact, first and steady-state steps, lengths with partial chunks and < 4 tails."""
+    from diloco_amd.kernels import default_kernels
+
+    k = default_kernels()
+    for n in (1, 3, 64, 4096 + 5, 3 * 4096 + 64 * 7 + 2):
+        g = torch.from_numpy(synth.values(5, n, n, 0.0, 1e-3))
+        if wire == torch.bfloat16:
+            g = g.to(torch.bfloat16).float()
+        th = synth.values(6, n, n, 0.0, 0.02)
+        buf = synth.values(7, n, n, 0.0, 1e-3)
+        dg, dth = g.to(DEV).to(wire), torch.from_numpy(th.copy()).to(DEV)
+        dm = torch.from_numpy(buf.copy()).to(DEV) if momentum else None
+        rth, rbuf = th.copy(), buf.copy()
+        for first in (True, False):
+            k.shard_sgd(dg, divisor, dth, dm, 0.7, momentum, nesterov, first)
+            gg = g.numpy().copy()
+            if divisor != 1:
+                gg = (gg / np.float32(divisor)).astype(np.float32)
+            oracle.sgd(rth, rbuf if momentum else None, gg, 0.7, momentum, nesterov, first)
+        torch.cuda.synchronize()
+        assert dth.cpu().numpy().tobytes() == rth.tobytes(), n
+        if momentum:
+            assert dm.cpu().numpy().tobytes() == rbuf.tobytes(), n
+
+
+def test_sharded_engine_single_rank_layout():
+    """The sharded engine's tree: buckets start at multiples of 64·n elements and split into n
+    equal shards; θ_outer starts as the inner params (a1)."""
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
+    e = OuterSync(params, world_size=4, bucket_cap_elems=4096, shard=True)
+    for lo, hi in e.tree.bucket_ranges:
+        assert lo % 256 == 0 and (hi - lo) % 256 == 0
+    assert e.shard_total * 4 == e.tree.total
+    assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == \
+        np.concatenate(_host(params)).tobytes()
+    e.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_sharded_step_emulated_matches_reference(n):
+    """The sharded variant of n replicas on one GPU, collectives emulated (reduce-scatter = sum
+    of the replicas' wire buckets, peer r keeps slice r; all-gather = concatenation of the θ
+    shards): θ, momentum and inner bit-exact vs the reference at n <= 2, normwise at n = 4."""
+    from conftest import normwise_ok
+
+    spec = get_tree("micro")
+    g = load_npz(f"micro_n{n}.npz")
+    theta0 = synth.outer_tree_device(spec, DEV)
+    shapes = [s for _, s in spec.params()]
+    engines, inners = [], []
+    for r in range(n):
+        inner = [t.clone().view(s) for t, s in zip(theta0, shapes)]
+        engines.append(OuterSync(inner, world_size=n, bucket_cap_elems=4096, shard=True, rank=r))
+        inners.append(inner)
+    e0 = engines[0]
+    assert e0.tree.n_buckets > 2
+    for s in (1, 2):
+        for r, (e, inner) in enumerate(zip(engines, inners)):
+            th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+            synth.inner_tree_device(th, s, r, out=[p.view(-1) for p in inner])
+        for b in range(e0.tree.n_buckets):
+            for e in engines:
+                e.pseudo_gradient(b)
+            total = engines[0].bucket_view(b).clone()
+            for e in engines[1:]:
+                total += e.bucket_view(b)
+            sl = e0._shard_len(b)
+            for r, e in enumerate(engines):
+                e._shard(e.g_shard, b).copy_(total[r * sl:(r + 1) * sl])
+                e.shard_apply(b)
+            gathered = torch.cat([e.th_shard_view(b) for e in engines])
+            lo, hi = e0.tree.bucket_ranges[b]
+            for e in engines:
+                e.theta[lo:hi].copy_(gathered)
+                e.write_inner(b)
+        for e in engines:
+            e.steps_done += 1
+        torch.cuda.synchronize()
+        mom = [torch.cat([e.mom_shard[e.shard_off[b]:e.shard_off[b] + e0._shard_len(b)]
+                          for e in engines]) for b in range(e0.tree.n_buckets)]
+        mom_full = torch.zeros_like(e0.theta)
+        for b, m in enumerate(mom):
+            lo, hi = e0.tree.bucket_ranges[b]
+            mom_full[lo:hi] = m
+        th = np.concatenate(_host(e0.unpacked(e0.theta)))
+        buf = np.concatenate(_host(e0.unpacked(mom_full)))
+        for e, inner in zip(engines, inners):
+            assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == th.tobytes()
+            assert np.concatenate(_host(inner)).tobytes() == th.tobytes()
+        if n <= 2:
+            assert th.tobytes() == g[f"theta_s{s}"].tobytes(), s
+            assert buf.tobytes() == g[f"buf_s{s}"].tobytes(), s
+        else:
+            numels = spec.numels()
+            for a, b in zip(split(th, numels), split(g[f"theta_s{s}"], numels)):
+                assert normwise_ok(a, b, 1e-6)
+            for a, b in zip(split(buf, numels), split(g[f"buf_s{s}"], numels)):
+                assert normwise_ok(a, b, 1e-6)
+
+
+def test_sharded_single_replica_without_process_group():
+    """shard=True, one replica, no process group: the collectives are local copies and the step
+    equals the reference's single-peer step bit-exact (momentum via momentum_full())."""
+    spec = get_tree("micro")
+    g = load_npz("micro_n1.npz")
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
+    e = OuterSync(params, world_size=1, bucket_cap_elems=4096, shard=True)
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        e.step()
+        torch.cuda.synchronize()
+        assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert np.concatenate(_host(e.unpacked(e.momentum_full()))).tobytes() == \
+            g[f"buf_s{s}"].tobytes()
+        assert np.concatenate(_host(params)).tobytes() == g[f"theta_s{s}"].tobytes()
+    e.close()

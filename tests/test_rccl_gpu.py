@@ -106,6 +106,20 @@ def _worker(rank, port, out):
     GradSync(gp, None, 1, bucket_cap_elems=4096).sync()
     torch.cuda.synchronize()
     rec["gradsync_equal"] = np.array([all(torch.equal(a, p.grad) for a, p in zip(before, gp))])
+    # 5. the sharded variant (reduce_scatter -> dl_shard_sgd -> all_gather -> dl_scatter)
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    sp = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+    es = OuterSync(sp, world_size=1, bucket_cap_elems=4096, shard=True)
+    assert es.sharded and es.tree.n_buckets > 2
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in es.unpacked(es.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in sp])
+        es.step()
+        torch.cuda.synchronize()
+        rec[f"sh_theta_s{s}"] = _flat(es.unpacked(es.theta))
+        rec[f"sh_buf_s{s}"] = _flat(es.unpacked(es.momentum_full()))
+        rec[f"sh_inner_s{s}"] = _flat(sp)
     np.savez(os.path.join(out, "rccl.npz"), **rec)
     dist.destroy_process_group()
 
@@ -123,6 +137,10 @@ def test_rccl_single_rank_transport_bit_exact():
     assert rec["t125_equal"][0]
     assert rec["bf16_equal"][0]
     assert rec["gradsync_equal"][0]
+    for s in (1, 2):
+        assert rec[f"sh_theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+        assert rec[f"sh_buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes()
+        assert rec[f"sh_inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
 
 
 def _worker_q8(rank, port, out):
