@@ -62,11 +62,17 @@ def setup_dist(n_gpus):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={ws}; launch N>1 with torchrun")
+    # DILOCO_BENCH_BACKEND=gloo rehearses the N > 1 code path with several ranks on one GPU
+    # (RCCL refuses two ranks per device); the driver's multi-GPU runs use RCCL.
+    backend = os.environ.get("DILOCO_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if ws > 1:
         # a hung collective becomes an error after 5 minutes instead of the 10-minute default
-        dist.init_process_group("nccl", device_id=dev, timeout=timedelta(minutes=5))
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, timeout=timedelta(minutes=5), **kw)
     return ws, rank, dev
 
 
@@ -261,7 +267,7 @@ def parity_sharded(dev, ws, rank):
             if s > 1:
                 th = [t.reshape(-1) for t in e.unpacked(e.theta)]
                 synth.inner_tree_device(th, s, rank, out=[p.view(-1) for p in e.params])
-            e.step(pipeline=True)
+            e.step()  # N = 1: local shard copies vs the two-kernel step
     torch.cuda.synchronize()
     worst, exact = 0.0, True
     ma, mb = ea.momentum_full(), eb.momentum_full()
