@@ -405,9 +405,10 @@ def parity_q8(dev, ws, rank):
             "replicas_identical": identical, "ok": bool(worst <= 1.0 and identical)}
 
 
-def dropin_rate(spec, dev, ws, rank, steps):
-    """The reference's call sequence (src/train.py:261-269) through the drop-in functions:
-    host-resident outer model, PCIe transfers included (DESIGN.md "Host-memory ends")."""
+def dropin_rate(spec, dev, ws, rank, steps, placement="host"):
+    """The reference's call sequence (src/train.py:261-269) through the drop-in functions.
+    placement "host": the reference's host-resident outer model, PCIe transfers included
+    (DESIGN.md "Host-memory ends"); "device": the outer model in HBM."""
     from types import SimpleNamespace
 
     from diloco_amd.comm import TrainingComm
@@ -424,7 +425,7 @@ def dropin_rate(spec, dev, ws, rank, steps):
     inner = torch.nn.Module()
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
-    outer = get_outer_model(inner)
+    outer = get_outer_model(inner, placement)
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
@@ -458,8 +459,11 @@ def dropin_rate(spec, dev, ws, rank, steps):
     return {"tree": spec.name, "value": round(ws * 4.0 * P / dt / 1e9, 2), "unit": "GB/s",
             "ms_per_step": round(dt * 1e3, 3),
             "phase_ms": {k: round(v / steps * 1e3, 3) for k, v in phases.items()},
-            "d2h_bytes_per_step": (16 if ws > 1 else 12) * P,
-            "note": "host outer model (reference semantics); D2H of delta, (avg,) θ, momentum"}
+            "placement": placement,
+            "d2h_bytes_per_step": ((16 if ws > 1 else 12) * P) if placement == "host" else 0,
+            "note": ("host outer model (reference semantics); D2H of delta, (avg,) θ, momentum"
+                     if placement == "host" else
+                     "outer model in HBM (params/.grad/momentum are packed views); no PCIe")}
 
 
 def gradsync_rate(spec, dev, ws, rank, steps):
@@ -581,6 +585,8 @@ def main():
                       "sharded": _guard(parity_sharded, dev, ws, rank)}
         if not a.no_dropin:
             dropin = _guard(dropin_rate, spec, dev, ws, rank, 5)
+            extra[f"{spec.name}_dropin_device"] = _guard(dropin_rate, spec, dev, ws, rank, 10,
+                                                         "device")
         if rank == 0 and ws == 1 and not a.no_cpu_baseline:
             log("timing the CPU baseline")
             cpu = cpu_baseline(spec)

@@ -138,9 +138,10 @@ class DPSync:
         params = list(model.parameters())
         if not params:
             return
-        if params[0].device.type == "cpu":
-            from .utils import outer_mirror
+        from .utils import _OUTER, outer_mirror
 
+        if params[0].device.type == "cpu" or getattr(model, _OUTER, False):
+            # an outer model (host or device placement): its packed mirror reduces in place
             m = outer_mirror(model)
             m.all_reduce(self.dp_group(m.device), num_peers)
             return

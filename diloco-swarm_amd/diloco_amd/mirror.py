@@ -209,3 +209,124 @@ class HostOuterMirror:
 
     def close(self) -> None:
         self.tree.close()
+
+
+class DeviceOuterMirror:
+    """Device-resident outer model: the outer parameters, their .grad and
+    the optimizer's momentum buffers ARE views into packed HBM arenas, so the reference's
+    compute_pseudo_gradient -> sync_gradients -> outer SGD -> sync_inner_model sequence runs
+    as dl_delta_pack -> RCCL all_reduce + dl_unpack_avg -> dl_unpack_sgd -> dl_scatter with no
+    host round trip and no host synchronisation (everything is ordered on the current stream).
+    A host copy is made only when asked for (`.cpu()`, `state_dict()`): torch copies lazily.
+
+    Chosen by get_outer_model(..., placement="device") or DILOCO_OUTER_PLACEMENT=device.
+    Tensors replaced by user code (p.data = ..., p.grad = ..., a loaded momentum buffer) are
+    detected by storage address and copied into the arenas before the next use."""
+
+    def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
+                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS):
+        self.params: List[torch.nn.Parameter] = list(outer_model.parameters())
+        if not self.params:
+            raise ValueError("outer model has no parameters")
+        self.k = kernels or default_kernels()
+        self.device = torch.device(device)
+        for i, p in enumerate(self.params):
+            if p.device != self.device:
+                raise ValueError(f"outer parameter {i} is on {p.device}, expected {self.device}")
+            if p.dtype != torch.float32:
+                raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
+        self.numels = [p.numel() for p in self.params]
+        self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems)
+        self.offs = [int(o) for o in self.tree.seg_off[:-1]]
+        z = dict(dtype=torch.float32, device=self.device)
+        self.d_theta = torch.zeros(self.tree.total, **z)
+        self.d_wire = torch.zeros(self.tree.total, **z)
+        self.d_mom: Optional[torch.Tensor] = None
+        self._relay(self.d_theta, "data")
+
+    def _view(self, arena: torch.Tensor, i: int) -> torch.Tensor:
+        o = self.offs[i]
+        return arena[o:o + self.numels[i]].view(self.params[i].shape)
+
+    def _relay(self, arena: torch.Tensor, what: str, zero_fill_missing: bool = True) -> None:
+        """Make every parameter's `what` ("data" or "grad") a view of `arena`."""
+        with torch.no_grad():
+            for i, p in enumerate(self.params):
+                v = self._view(arena, i)
+                cur = p.data if what == "data" else p.grad
+                if cur is not None and cur.data_ptr() == v.data_ptr():
+                    continue
+                if cur is None:
+                    if not zero_fill_missing:
+                        raise RuntimeError(
+                            f"outer parameter {i} has no gradient: the fused outer step updates "
+                            "every tensor (call compute_pseudo_gradient first)")
+                    v.zero_()  # src/comm.py:121: zeros_like(param)
+                else:
+                    v.copy_(cur)
+                if what == "data":
+                    p.data = v
+                else:
+                    p.grad = v
+
+    def invalidate(self) -> None:  # the arenas are the tensors: nothing is cached
+        pass
+
+    # ---- the four reference operations --------------------------------------------------
+    def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
+        """outer.grad = outer - inner (src/utils.py:218-221); .grad are views of d_wire."""
+        self._relay(self.d_theta, "data")
+        self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
+        self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
+        for i, p in enumerate(self.params):
+            v = self._view(self.d_wire, i)
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+
+    def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
+        """grad = Σ_peers grad / n (src/comm.py:120-123), in place on the packed .grad."""
+        self._relay(self.d_wire, "grad", zero_fill_missing=True)
+
+        def view(b):
+            lo, hi = self.tree.bucket_ranges[b]
+            return self.d_wire[lo:hi]
+
+        pipelined_buckets(
+            self.tree.n_buckets, lambda b: None,
+            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
+            lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
+        )
+
+    def sgd_step(self, lr: float, momentum: float, nesterov: bool,
+                 host_bufs: Optional[List[Optional[torch.Tensor]]]) -> List[Optional[torch.Tensor]]:
+        """torch.optim.SGD._single_tensor_sgd over the whole tree; returns the momentum
+        buffers (views of d_mom) for the optimizer state."""
+        self._relay(self.d_theta, "data")
+        self._relay(self.d_wire, "grad", zero_fill_missing=False)
+        first = True
+        bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
+        if momentum != 0:
+            if self.d_mom is None:
+                self.d_mom = torch.zeros_like(self.d_theta)
+            have = [b is not None for b in host_bufs]
+            if any(have) and not all(have):
+                raise RuntimeError("momentum buffers exist for some outer parameters only")
+            first = not any(have)
+            bufs = [self._view(self.d_mom, i) for i in range(len(self.params))]
+            if not first:
+                with torch.no_grad():
+                    for b, v in zip(host_bufs, bufs):
+                        if b.data_ptr() != v.data_ptr():
+                            v.copy_(b)  # e.g. a state_dict loaded into the optimizer
+        self.k.unpack_sgd(self.tree, ALL, self.d_wire, 1, self.d_theta,
+                          self.d_mom if momentum != 0 else None, lr, momentum, nesterov, first, -1)
+        return bufs
+
+    def copy_to_inner(self, inner_params: Sequence[torch.Tensor]) -> None:
+        """inner = outer (src/utils.py:223-226), scattered from HBM."""
+        self._relay(self.d_theta, "data")
+        self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
+        self.k.scatter(self.tree, ALL, self.d_theta, SLOT_INNER)
+
+    def close(self) -> None:
+        self.tree.close()

@@ -7,31 +7,50 @@ Same names, arguments and host-visible results as the reference; the work runs o
   sync_inner_model(out, in)         in = out              (dl_scatter)      src/utils.py:223-226
   get_optimizer(model, cfg)         AdamW | SGD (outer: OuterSGD, HIP)      src/utils.py:59-65
 
-The outer model stays a CPU module whose parameters, gradients and momentum buffers hold
-exactly the reference's values; a device mirror (mirror.HostOuterMirror) is attached to it on
-first use and keeps the packed copies in HBM coherent with the host tensors.
+Placement of the outer model (`get_outer_model(..., placement=)`, default from the
+DILOCO_OUTER_PLACEMENT environment variable, "host" if unset):
+
+  "host"    the reference's placement: a CPU module whose parameters, gradients and momentum
+            buffers hold exactly the reference's values; a device mirror
+            (mirror.HostOuterMirror) keeps packed copies in HBM coherent with them (one
+            pinned DMA per arena per step).
+  "device"  SURVEY §8f row 2: the outer module lives on the inner model's GPU, its parameters,
+            .grad and momentum buffers are views of packed HBM arenas
+            (mirror.DeviceOuterMirror); no PCIe traffic and no host synchronisation per outer
+            step. Host copies are made lazily by torch (`.cpu()`, `state_dict()`).
 """
 from __future__ import annotations
 
 import copy
+import os
 
 import torch
 import torch.nn as nn
 from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
-from .mirror import HostOuterMirror
+from .mirror import DeviceOuterMirror, HostOuterMirror
 from .optim import OuterSGD
 
 _ATTR = "_diloco_mirror"
 _OUTER = "_diloco_outer"
+_PLACEMENT = "_diloco_placement"
+PLACEMENTS = ("host", "device")
 
 
-def outer_mirror(outer_model: nn.Module, device=None) -> HostOuterMirror:
-    """The device mirror of a host outer model (created on first use)."""
+def outer_mirror(outer_model: nn.Module, device=None):
+    """The device mirror of an outer model (created on first use): HostOuterMirror for the
+    reference's host placement, DeviceOuterMirror for placement="device"."""
     m = getattr(outer_model, _ATTR, None)
     if m is None:
         k = default_kernels()
+        if getattr(outer_model, _PLACEMENT, "host") == "device":
+            p = next(outer_model.parameters(), None)
+            if p is None:
+                raise ValueError("outer model has no parameters")
+            m = DeviceOuterMirror(outer_model, p.device, kernels=k)
+            object.__setattr__(outer_model, _ATTR, m)
+            return m
         if device is None:
             device = getattr(k, "default_device", None)
             if device is None:
@@ -50,11 +69,31 @@ def _inner_device(inner_model: nn.Module) -> torch.device:
     return p.device
 
 
-def get_outer_model(inner_model: nn.Module) -> nn.Module:
-    """Initializes the outer model from the inner model (src/utils.py:213-216)."""
+def get_outer_model(inner_model: nn.Module, placement: str = None) -> nn.Module:
+    """Initializes the outer model from the inner model (src/utils.py:213-216).
+
+    placement "host" (the reference's, default) or "device" (see the module docstring)."""
+    if placement is None:
+        placement = os.environ.get("DILOCO_OUTER_PLACEMENT", "host")
+    if placement not in PLACEMENTS:
+        raise ValueError(f"placement {placement!r}: one of {PLACEMENTS}")
     outer_model = copy.deepcopy(inner_model)
-    outer_model = outer_model.to("cpu")
+    if placement == "host":
+        outer_model = outer_model.to("cpu")
+    else:  # the inner model's GPU; the reference builds the outer model before moving the
+        # inner one (src/train.py:382), so a CPU inner model means the current device
+        dev = _inner_device(inner_model)
+        if dev.type == "cpu":
+            dev = getattr(default_kernels(), "default_device", None)
+            if dev is None:
+                if not torch.cuda.is_available():
+                    raise RuntimeError("placement='device' needs a HIP device")
+                dev = torch.device("cuda", torch.cuda.current_device())
+        outer_model = outer_model.to(dev)
     object.__setattr__(outer_model, _OUTER, True)  # get_optimizer: SGD here is the outer SGD
+    object.__setattr__(outer_model, _PLACEMENT, placement)
+    if placement == "device":
+        outer_mirror(outer_model)  # lay the parameters out in the packed HBM arena now
     return outer_model
 
 

@@ -69,11 +69,14 @@ def _worker(rank, world, port, mode, num_stages, out):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
     rec = {}
-    if mode == "dropin":
+    if mode in ("dropin", "dropin_device"):
         inner = _micro_module(theta0, shapes)
-        outer = get_outer_model(inner)
+        outer = get_outer_model(inner, placement="device" if mode == "dropin_device" else None)
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
         assert type(opt).__name__ == "OuterSGD"
+        from diloco_amd.utils import outer_mirror
+        assert type(outer_mirror(outer)).__name__ == (
+            "DeviceOuterMirror" if mode == "dropin_device" else "HostOuterMirror")
         comm = TrainingComm(world_, (1, 1, 32), None)
         for s in range(1, MICRO_STEPS + 1):
             prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
@@ -156,7 +159,7 @@ def _run(mode, world, num_stages=1):
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "engine", "engine_ar"])
+@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "engine", "engine_ar"])
 def test_two_peers_match_reference_bit_exact(mode):
     g = load_npz("micro_n2.npz")
     recs = _run(mode, 2)
@@ -165,9 +168,9 @@ def test_two_peers_match_reference_bit_exact(mode):
             for k in ("theta", "buf"):
                 assert rec[f"{k}_s{s}"].tobytes() == g[f"{k}_s{s}"].tobytes(), (mode, k, s)
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
-            if mode == "dropin":
+            if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
-    if mode == "dropin":
+    if mode.startswith("dropin"):
         assert recs[0]["delta_s1"].tobytes() == g["delta_s1_r0"].tobytes()
         assert recs[1]["delta_s1"].tobytes() == g["delta_s1_rlast"].tobytes()
 

@@ -48,7 +48,7 @@ def _flat(ts):
     return np.concatenate([t.detach().cpu().numpy().reshape(-1) for t in ts])
 
 
-def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0):
+def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=None):
     """The reference's outer step sequence with the drop-in functions (this process = DP
     rank `rank` of `n`; the default process group must exist)."""
     from diloco_amd import synth
@@ -61,8 +61,10 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0):
     spec = get_tree("micro")
     shapes = [s for _, s in spec.params()]
     inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cpu")
-    outer = get_outer_model(inner)  # src/train.py:382: before the inner model moves
+    outer = get_outer_model(inner, placement)  # src/train.py:382: before the inner model moves
     inner = inner.to("cuda:0")
+    if placement == "device":
+        assert all(p.is_cuda for p in outer.parameters())
     if stock_sgd:
         opt = torch.optim.SGD(outer.parameters(), lr=0.7, momentum=0.9, nesterov=True)
     else:
@@ -71,7 +73,7 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0):
     comm = TrainingComm(World.from_default_group(1), (1, 1, 32), None)
     rec = {}
     for s in range(1, steps + 1):
-        prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
+        prev = [p.detach().cpu().numpy().reshape(-1).copy() for p in outer.parameters()]
         vals = synth.inner_tree(prev, s, rank)
         with torch.no_grad():
             for p, v in zip(inner.parameters(), vals):
@@ -100,11 +102,15 @@ def _init_single():
         dist.init_process_group("gloo", init_method=f"file://{f}", rank=0, world_size=1)
 
 
-@pytest.mark.parametrize("stock_sgd", [False, True])
-def test_dropin_single_peer_matches_reference(stock_sgd):
+@pytest.mark.parametrize("stock_sgd,placement", [(False, "host"), (True, "host"),
+                                                 (False, "device")])
+def test_dropin_single_peer_matches_reference(stock_sgd, placement):
+    """The reference's call sequence, outer model on the host (its placement) or in HBM
+    (placement="device"); torch's own CPU SGD on the host outer model as
+    well (the mirror must see its in-place updates)."""
     _init_single()
     g = load_npz("micro_n1.npz")
-    rec = _outer_steps(0, 1, stock_sgd=stock_sgd)
+    rec = _outer_steps(0, 1, stock_sgd=stock_sgd, placement=placement)
     for s in (1, 2):
         assert rec[f"delta_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()
         assert rec[f"avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()  # n=1: no sync
@@ -159,8 +165,8 @@ def _worker(rank, world, port, mode, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     rec = {}
-    if mode == "dropin":
-        rec = _outer_steps(rank, world)
+    if mode in ("dropin", "dropin_device"):
+        rec = _outer_steps(rank, world, placement="device" if mode == "dropin_device" else None)
     elif mode in ("engine", "engine_ar"):
         from diloco_amd import synth
         from diloco_amd.outer import OuterSync
@@ -213,7 +219,7 @@ def _run(mode, world=2):
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "engine", "engine_ar"])
+@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "engine", "engine_ar"])
 def test_two_peers_on_gpu_match_reference(mode):
     g = load_npz("micro_n2.npz")
     for rec in _run(mode):
@@ -221,7 +227,7 @@ def test_two_peers_on_gpu_match_reference(mode):
             assert rec[f"theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
             assert rec[f"buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes(), (mode, s)
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
-            if mode == "dropin":
+            if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
 
 
