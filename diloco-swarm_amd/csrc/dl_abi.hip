@@ -67,6 +67,10 @@ int plan(const int64_t* numel, int32_t n, int64_t cap, int32_t align, int64_t bu
 
 }  // namespace
 
+namespace dl {
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+}  // namespace dl
+
 struct dl_tree_s {
   int device = 0;
   int32_t nseg = 0;

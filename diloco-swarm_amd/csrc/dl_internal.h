@@ -41,6 +41,9 @@ struct Launch {
   hipStream_t stream;
 };
 
+// dl_last_error() text for entry points outside dl_abi.hip; returns `code`
+int set_error(int code, const char* msg);
+
 hipError_t launch_delta_pack(const Launch& L, int inner_slot, const float* outer, void* wire,
                              int wire_dtype);
 hipError_t launch_unpack_avg(const Launch& L, const void* wire, int wire_dtype, int divisor,

@@ -21,7 +21,7 @@ CHUNK_ELEMS = 4096
 ALL_BUCKETS = -1
 MAX_SLOTS = 4
 Q8_SLOT_BYTES = 4160
-DL_F32, DL_BF16, DL_F16 = 0, 1, 2
+DL_F32, DL_BF16, DL_F16, DL_U8 = 0, 1, 2, 3
 TUNE_NT_LOADS, TUNE_NT_STORES = 1, 2
 TUNE_AUTO = -1
 
@@ -63,6 +63,14 @@ SIGNATURES = {
     "dl_scatter": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp]),
     "dl_serialize": (ctypes.c_int, [_vp, _i32, _i64, _f32, _f32, _vp, _vp]),
     "dl_fill_synth": (ctypes.c_int, [_vp, _i64, _u64, _u64, _f32, _f32, _vp, _vp]),
+    "dl_rccl_load": (ctypes.c_int, [ctypes.c_char_p]),
+    "dl_rccl_version": (ctypes.c_int, [_pi32]),
+    "dl_comm_unique_id": (ctypes.c_int, [_vp]),
+    "dl_comm_init": (ctypes.c_int, [ctypes.POINTER(_vp), _i32, _vp, _i32]),
+    "dl_comm_destroy": (ctypes.c_int, [_vp]),
+    "dl_allreduce": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
+    "dl_reduce_scatter": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "dl_all_gather": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "dl_last_error": (ctypes.c_char_p, []),
     "dl_abi_version": (ctypes.c_int, []),
 }

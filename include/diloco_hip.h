@@ -41,15 +41,18 @@ extern "C" {
 #define DL_F32 0
 #define DL_BF16 1
 #define DL_F16 2
+#define DL_U8 3 /* bytes (int8 wire slots); collectives only */
 
 /* errors (negative); positive codes are hipError_t */
 #define DL_OK 0
 #define DL_E_ARG (-1)
 #define DL_E_STATE (-2)
 #define DL_E_ALIGN (-3)
+#define DL_E_RCCL (-4) /* an RCCL call failed; dl_last_error() has its message */
 
 typedef struct dl_tree_s* dl_tree_t;
 typedef void* dl_stream_t; /* hipStream_t */
+typedef void* dl_comm_t;   /* ncclComm_t of the RCCL selected by dl_rccl_load */
 
 /* ---- planner (host only; needs no GPU) -------------------------------------------------
  * Replaces the reference's implicit layout: the per-tensor loop over model.parameters()
@@ -187,6 +190,29 @@ DL_API int dl_serialize(const void* src, int32_t src_dtype, int64_t numel, float
  * all fp32 ops correctly rounded: bit-identical to diloco_amd.synth (numpy). */
 DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id, float base,
                          float scale, const float* add, dl_stream_t stream);
+
+/* ---- RCCL ------------------------------------------------------------
+ * The exchange of src/comm.py:122 for hosts that drive RCCL through this library instead of
+ * torch.distributed. RCCL is resolved at run time: a communicator must be used with the
+ * RCCL that created it (a PyTorch process carries its own; ProcessGroupNCCL._comm_ptr()
+ * returns its ncclComm_t). dl_rccl_load(path): that library; NULL = the RCCL already loaded
+ * in the process, else librccl.so.1. The other entry points load it on first use.
+ * Collectives are SUM, enqueued on `stream`, dtype DL_F32 / DL_BF16 / DL_F16 / DL_U8. */
+DL_API int dl_rccl_load(const char* path);
+DL_API int dl_rccl_version(int32_t* version);
+DL_API int dl_comm_unique_id(void* id /* 128 B, NCCL_UNIQUE_ID_BYTES */);
+DL_API int dl_comm_init(dl_comm_t* comm, int32_t nranks, const void* id, int32_t rank);
+DL_API int dl_comm_destroy(dl_comm_t comm);
+/* in place: buf[0:count) <- Σ over the communicator's ranks (src/comm.py:122; /n is the
+ * caller's, e.g. dl_unpack_sgd's divisor) */
+DL_API int dl_allreduce(void* buf, int64_t count, int32_t dtype, dl_comm_t comm,
+                        dl_stream_t stream);
+/* recv[0:recv_count) <- Σ_ranks send[rank*recv_count : (rank+1)*recv_count) (sharded step) */
+DL_API int dl_reduce_scatter(const void* send, void* recv, int64_t recv_count, int32_t dtype,
+                             dl_comm_t comm, dl_stream_t stream);
+/* recv[r*send_count : (r+1)*send_count) <- rank r's send[0:send_count) */
+DL_API int dl_all_gather(const void* send, void* recv, int64_t send_count, int32_t dtype,
+                         dl_comm_t comm, dl_stream_t stream);
 
 DL_API const char* dl_last_error(void);
 DL_API int dl_abi_version(void);

@@ -143,3 +143,18 @@ def test_bucket_aligned_planner_fuzz_and_properties():
     check()
     with pytest.raises(_lib.DilocoHipError):
         plan_tables([1, 2], 0, 64, 96)  # not a multiple of align
+
+
+def test_rccl_entry_points_resolve_and_fail_loudly():
+    """The C-ABI's RCCL layer loads RCCL at run time (no GPU needed for that) and reports a bad
+    library path or a null communicator as an error, never a crash."""
+    from diloco_amd import rccl
+
+    with pytest.raises(_lib.DilocoHipError, match="cannot open"):
+        rccl.load("/nonexistent/librccl.so")
+    rccl.load(None)
+    assert rccl.version() >= 20000  # NCCL_VERSION_CODE of RCCL 2.x
+    with pytest.raises(_lib.DilocoHipError, match="null communicator"):
+        _lib.call("dl_allreduce", None, 0, _lib.DL_F32, None, None)
+    with pytest.raises(_lib.DilocoHipError, match="unsupported dtype"):
+        _lib.call("dl_all_gather", None, None, 0, 7, 1, None)

@@ -182,3 +182,78 @@ def test_rccl_single_rank_int8_exchange():
     exp = expected_q8(1)
     for s in (1, 2):
         assert rec[f"theta_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes()
+
+
+def _worker_cabi(rank, port, out):
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from datetime import timedelta
+
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                            timeout=timedelta(seconds=120))
+    from diloco_amd import _lib, rccl, synth
+    from diloco_amd.kernels import default_kernels
+    from diloco_amd.plan import SLOT_INNER
+    from diloco_amd.trees import get_tree
+
+    rec = {}
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(100_003, generator=g).to(dev)
+    for name, comm in (("torch", rccl.Comm.from_process_group(None, dev)),
+                       ("own", rccl.Comm.create(1, 0, rccl.Comm.unique_id()))):
+        a, b = x.clone(), x.to(torch.bfloat16)
+        comm.all_reduce(a)
+        comm.all_reduce(b)
+        rs, ag = torch.empty_like(x), torch.empty_like(x)
+        comm.reduce_scatter(rs, x)
+        comm.all_gather(ag, rs)
+        torch.cuda.synchronize()
+        rec[f"{name}_identity"] = np.array([
+            torch.equal(a, x) and torch.equal(b, x.to(torch.bfloat16)) and torch.equal(rs, x)
+            and torch.equal(ag, x)])
+        comm.close()
+    # the outer step through the C-ABI alone: dl_delta_pack -> dl_allreduce per bucket ->
+    # dl_unpack_sgd (divisor 1: one peer), on torch's communicator
+    comm = rccl.Comm.from_process_group(None, dev)
+    k = default_kernels()
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)]
+    tree = k.tree(spec.numels(), dev, 4096)
+    k.bind(tree, SLOT_INNER, params, dev)
+    theta = torch.zeros(tree.total, device=dev)
+    mom = torch.zeros_like(theta)
+    wire = torch.zeros_like(theta)
+    k.gather(tree, _lib.ALL_BUCKETS, SLOT_INNER, theta)
+    for s in (1, 2):
+        th = [theta[int(o):int(o) + n] for o, n in zip(tree.seg_off[:-1], spec.numels())]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        for b in range(tree.n_buckets):
+            lo, hi = tree.bucket_ranges[b]
+            k.delta_pack(tree, b, SLOT_INNER, theta, wire)
+            comm.all_reduce(wire[lo:hi])
+            k.unpack_sgd(tree, b, wire, 1, theta, mom, 0.7, 0.9, True, s == 1, SLOT_INNER)
+        torch.cuda.synchronize()
+        rec[f"cabi_theta_s{s}"] = _flat(params)
+    rec["buckets"] = np.array([tree.n_buckets])
+    tree.close()
+    np.savez(os.path.join(out, "cabi.npz"), **rec)
+    dist.destroy_process_group()
+
+
+def test_rccl_through_the_c_abi():
+    """dl_allreduce / dl_reduce_scatter / dl_all_gather on torch's communicator and on one the
+    library creates (identity at one rank), and a whole outer step driven through the C-ABI
+    only, bit-exact vs the reference."""
+    out = tempfile.mkdtemp(prefix="dl_cabi_")
+    mp.spawn(_worker_cabi, args=(_free_port(), out), nprocs=1, join=True)
+    rec = dict(np.load(os.path.join(out, "cabi.npz")))
+    assert rec["torch_identity"][0] and rec["own_identity"][0]
+    assert rec["buckets"][0] > 2
+    g = load_npz("micro_n1.npz")
+    for s in (1, 2):
+        assert rec[f"cabi_theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
