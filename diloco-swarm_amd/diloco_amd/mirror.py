@@ -242,17 +242,36 @@ class DeviceOuterMirror:
         self.d_theta = torch.zeros(self.tree.total, **z)
         self.d_wire = torch.zeros(self.tree.total, **z)
         self.d_mom: Optional[torch.Tensor] = None
-        self._relay(self.d_theta, "data")
+        # per-tensor views of each arena and their addresses, made once: the per-step checks
+        # compare raw addresses (an outer step must not cost a Python tensor per parameter)
+        self._views = {"theta": self._make_views(self.d_theta),
+                       "wire": self._make_views(self.d_wire)}
+        self._ptrs = {k: [v.data_ptr() for v in vs] for k, vs in self._views.items()}
+        self._relay("theta", "data")
+
+    def _make_views(self, arena: torch.Tensor) -> List[torch.Tensor]:
+        return [arena[o:o + n].view(p.shape)
+                for o, n, p in zip(self.offs, self.numels, self.params)]
 
     def _view(self, arena: torch.Tensor, i: int) -> torch.Tensor:
         o = self.offs[i]
         return arena[o:o + self.numels[i]].view(self.params[i].shape)
 
-    def _relay(self, arena: torch.Tensor, what: str, zero_fill_missing: bool = True) -> None:
-        """Make every parameter's `what` ("data" or "grad") a view of `arena`."""
+    def _in_place(self, kind: str, what: str) -> bool:
+        exp = self._ptrs[kind]
+        if what == "data":
+            return all(p.data_ptr() == e for p, e in zip(self.params, exp))
+        return all(p.grad is not None and p.grad.data_ptr() == e
+                   for p, e in zip(self.params, exp))
+
+    def _relay(self, kind: str, what: str, zero_fill_missing: bool = True) -> None:
+        """Make every parameter's `what` ("data" or "grad") the view of arena `kind`."""
+        if self._in_place(kind, what):
+            return
+        views = self._views[kind]
         with torch.no_grad():
             for i, p in enumerate(self.params):
-                v = self._view(arena, i)
+                v = views[i]
                 cur = p.data if what == "data" else p.grad
                 if cur is not None and cur.data_ptr() == v.data_ptr():
                     continue
@@ -275,17 +294,17 @@ class DeviceOuterMirror:
     # ---- the four reference operations --------------------------------------------------
     def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
         """outer.grad = outer - inner (src/utils.py:218-221); .grad are views of d_wire."""
-        self._relay(self.d_theta, "data")
-        self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
+        self._relay("theta", "data")
+        self.k.bind(self.tree, SLOT_INNER, inner_params, self.device)
         self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
-        for i, p in enumerate(self.params):
-            v = self._view(self.d_wire, i)
-            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
-                p.grad = v
+        if not self._in_place("wire", "grad"):
+            for p, v, e in zip(self.params, self._views["wire"], self._ptrs["wire"]):
+                if p.grad is None or p.grad.data_ptr() != e:
+                    p.grad = v
 
     def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
         """grad = Σ_peers grad / n (src/comm.py:120-123), in place on the packed .grad."""
-        self._relay(self.d_wire, "grad", zero_fill_missing=True)
+        self._relay("wire", "grad", zero_fill_missing=True)
 
         def view(b):
             lo, hi = self.tree.bucket_ranges[b]
@@ -301,22 +320,24 @@ class DeviceOuterMirror:
                  host_bufs: Optional[List[Optional[torch.Tensor]]]) -> List[Optional[torch.Tensor]]:
         """torch.optim.SGD._single_tensor_sgd over the whole tree; returns the momentum
         buffers (views of d_mom) for the optimizer state."""
-        self._relay(self.d_theta, "data")
-        self._relay(self.d_wire, "grad", zero_fill_missing=False)
+        self._relay("theta", "data")
+        self._relay("wire", "grad", zero_fill_missing=False)
         first = True
         bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
         if momentum != 0:
             if self.d_mom is None:
                 self.d_mom = torch.zeros_like(self.d_theta)
+                self._views["mom"] = self._make_views(self.d_mom)
+                self._ptrs["mom"] = [v.data_ptr() for v in self._views["mom"]]
             have = [b is not None for b in host_bufs]
             if any(have) and not all(have):
                 raise RuntimeError("momentum buffers exist for some outer parameters only")
             first = not any(have)
-            bufs = [self._view(self.d_mom, i) for i in range(len(self.params))]
+            bufs = self._views["mom"]
             if not first:
                 with torch.no_grad():
-                    for b, v in zip(host_bufs, bufs):
-                        if b.data_ptr() != v.data_ptr():
+                    for b, v, e in zip(host_bufs, bufs, self._ptrs["mom"]):
+                        if b.data_ptr() != e:
                             v.copy_(b)  # e.g. a state_dict loaded into the optimizer
         self.k.unpack_sgd(self.tree, ALL, self.d_wire, 1, self.d_theta,
                           self.d_mom if momentum != 0 else None, lr, momentum, nesterov, first, -1)
@@ -324,8 +345,8 @@ class DeviceOuterMirror:
 
     def copy_to_inner(self, inner_params: Sequence[torch.Tensor]) -> None:
         """inner = outer (src/utils.py:223-226), scattered from HBM."""
-        self._relay(self.d_theta, "data")
-        self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
+        self._relay("theta", "data")
+        self.k.bind(self.tree, SLOT_INNER, inner_params, self.device)
         self.k.scatter(self.tree, ALL, self.d_theta, SLOT_INNER)
 
     def close(self) -> None:
