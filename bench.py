@@ -576,6 +576,10 @@ def main():
             r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, cap, False,
                        False, False)
             extra[f"{spec.name}_allreduce_variant"] = _brief(r) if "value" in r else r
+            # bucket size for the xGMI pipeline: 64 MiB buckets (more overlap, more calls)
+            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, 16 << 20, False,
+                       False)
+            extra[f"{spec.name}_bucket64MiB"] = _brief(r) if "value" in r else r
             extra[f"{spec.name}_dp_grad_sync"] = _guard(gradsync_rate, spec, dev, ws, rank,
                                                         max(3, a.steps // 2))
         if not a.no_parity:
