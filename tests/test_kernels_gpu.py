@@ -536,3 +536,45 @@ def test_sharded_single_replica_without_process_group():
             g[f"buf_s{s}"].tobytes()
         assert np.concatenate(_host(params)).tobytes() == g[f"theta_s{s}"].tobytes()
     e.close()
+
+
+def test_sharded_bf16_wire_equals_replicated_bf16_wire():
+    """bf16 wire, n = 2 emulated on one GPU: reduce-scatter (sum of two bf16 values, rounded to
+    bf16 as RCCL does) -> dl_shard_sgd equals all-reduce -> dl_unpack_sgd bit-exact."""
+    spec = get_tree("micro")
+    n = 2
+    rep, rep_in = _engines(spec, n, wire=torch.bfloat16, cap=4096)
+    theta0 = synth.outer_tree_device(spec, DEV)
+    shapes = [s for _, s in spec.params()]
+    sh, sh_in = [], []
+    for r in range(n):
+        inner = [t.clone().view(s) for t, s in zip(theta0, shapes)]
+        sh.append(OuterSync(inner, world_size=n, wire_dtype=torch.bfloat16, bucket_cap_elems=4096,
+                            shard=True, rank=r))
+        sh_in.append(inner)
+    for s in (1, 2):
+        _emulated_step(rep, rep_in, s, per_bucket=True)
+        for r, (e, inner) in enumerate(zip(sh, sh_in)):
+            th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+            synth.inner_tree_device(th, s, r, out=[p.view(-1) for p in inner])
+        e0 = sh[0]
+        for b in range(e0.tree.n_buckets):
+            for e in sh:
+                e.pseudo_gradient(b)
+            total = sh[0].bucket_view(b) + sh[1].bucket_view(b)  # bf16 + bf16 -> bf16
+            sl = e0._shard_len(b)
+            for r, e in enumerate(sh):
+                e._shard(e.g_shard, b).copy_(total[r * sl:(r + 1) * sl])
+                e.shard_apply(b)
+            gathered = torch.cat([e.th_shard_view(b) for e in sh])
+            lo, hi = e0.tree.bucket_ranges[b]
+            for e in sh:
+                e.theta[lo:hi].copy_(gathered)
+                e.write_inner(b)
+        for e in sh:
+            e.steps_done += 1
+        torch.cuda.synchronize()
+        want = np.concatenate(_host(rep[0].unpacked(rep[0].theta)))
+        for e, inner in zip(sh, sh_in):
+            assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == want.tobytes(), s
+            assert np.concatenate(_host(inner)).tobytes() == want.tobytes(), s

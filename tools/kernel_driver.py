@@ -31,6 +31,14 @@ def main():
     fused.step()
     for _ in range(reps):
         fused.step()
+    # one bucket each, so every launch covers the whole tree: the int8 wire kernels and the
+    # sharded step's dl_shard_sgd (one replica: the shard is the whole bucket)
+    q8 = OuterSync(params, world_size=1, wire_dtype=torch.int8, bucket_cap_elems=0)
+    sh = OuterSync(params, world_size=1, shard=True, bucket_cap_elems=0)
+    for e in (q8, sh):
+        assert e.tree.n_buckets == 1
+        for _ in range(reps + 1):
+            e.step()
     torch.cuda.synchronize()
     print(f"kernel_driver: {tree} x{reps} done")
 
