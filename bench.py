@@ -491,6 +491,52 @@ def gradsync_rate(spec, dev, ws, rank, steps):
             "ms_per_step": round(dt * 1e3, 4), "buckets": gs.tree.n_buckets}
 
 
+def p2p_rate(spec, dev, ws, rank, steps):
+    """Device p2p transport (src/comm.py:16-69): two stages (rank % 2),
+    stage-0 rank r sends a framed (2, mbs, seq, n_embd) activation to r+1 and gets it back;
+    header over gloo, payload over RCCL data groups. Opt-in (--p2p)."""
+    from diloco_amd.p2p import DeviceRecvThread, DeviceSendThread, boundary_data_groups
+    from diloco_amd.world import World
+
+    if ws < 2 or ws % 2:
+        return {"ok": False, "error": "needs an even number of ranks >= 2"}
+    w = World.from_default_group(2)  # the reference's stage groups (gloo)
+    dg = boundary_data_groups(w, backend=dist.get_backend())
+    shape = (8, 1024, spec.n_embd)  # mbs 8, seq 1024 (SURVEY §8f row 3 activations)
+    kw = dict(start=False, serialize=True)
+    if w.stage == 0:
+        tx = DeviceSendThread(shape, w.next_stage_group, dg[(0, 1, "fwd")], dev, **kw)
+        rx = DeviceRecvThread(shape, w.next_stage_group, dg[(0, 1, "bwd")], dev, **kw)
+    else:
+        tx = DeviceSendThread(shape, w.prev_stage_group, dg[(0, 1, "bwd")], dev, **kw)
+        rx = DeviceRecvThread(shape, w.prev_stage_group, dg[(0, 1, "fwd")], dev, **kw)
+    act = torch.randn(shape, device=dev)
+    ok = True
+
+    def round_trip(i):
+        nonlocal ok
+        if w.stage == 0:
+            tx.send_one(rank + 1, act, (rank, i))
+            src, t, meta = rx.recv_one()
+            ok &= src == rank + 1 and meta == (rank, i)
+        else:
+            src, t, meta = rx.recv_one()
+            ok &= src == rank - 1 and meta == (src, i)
+            tx.send_one(src, t.detach(), meta)
+
+    round_trip(-1)
+    _sync(ws)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        round_trip(i)
+    _sync(ws)
+    dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
+    frame = 2 * act.numel() * 4
+    return {"frame_bytes": frame, "ms_per_round_trip": round(dt * 1e3, 4),
+            "value": round(2 * frame / dt / 1e9, 2), "unit": "GB/s per rank pair",
+            "transport": f"header gloo, payload {dist.get_backend()}", "ok": bool(ok)}
+
+
 def cpu_baseline(spec, seconds_budget=12.0):
     """The reference's per-tensor CPU sequence (oracle/torch_restatement.py), 1 thread."""
     sys.path.insert(0, HERE)
@@ -542,6 +588,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the host-outer-model rate")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--p2p", action="store_true",
+                    help="also time the device p2p transport (N even; SURVEY §8f row 3)")
     ap.add_argument("--only-headline", action="store_true",
                     help="headline tree only (for rocprofv3 runs of the same kernels)")
     ap.add_argument("--no-b2b", action="store_true",
@@ -587,6 +635,8 @@ def main():
                       "bf16": _guard(parity_check, dev, ws, rank, torch.bfloat16),
                       "int8": _guard(parity_q8, dev, ws, rank),
                       "sharded": _guard(parity_sharded, dev, ws, rank)}
+        if a.p2p:
+            extra["p2p_device_transport"] = _guard(p2p_rate, spec, dev, ws, rank, 10)
         if not a.no_dropin:
             dropin = _guard(dropin_rate, spec, dev, ws, rank, 5)
             extra[f"{spec.name}_dropin_device"] = _guard(dropin_rate, spec, dev, ws, rank, 10,

@@ -168,17 +168,50 @@ def dp_sync_gradients(world, model: nn.Module) -> None:
 
 
 class TrainingComm:
-    def __init__(self, world, shape: Tuple[int, ...], logger):
+    """src/comm.py:71-149. `transport` (default: DILOCO_P2P_TRANSPORT, else "host") selects the
+    pipeline p2p threads: "host" = the reference's (frame, copy to host, gloo send/recv);
+    "device" = p2p.DeviceSendThread / DeviceRecvThread (GPU framing, header over the same gloo
+    group, payload over per-direction RCCL data groups)."""
+
+    def __init__(self, world, shape: Tuple[int, ...], logger, transport: Optional[str] = None,
+                 device: Optional[torch.device] = None, serializer_factory=None):
         self.world, self.shape, self.logger = world, shape, logger
         kw = {"tag": 0, "serialize": True, "requires_grad": True, "logger": logger}
-        self.forward_send_thread = SendThread(shape, group=world.next_stage_group,
-                                              start=world.has_next_stage, **kw)
-        self.backward_recv_thread = RecvThread(shape, group=world.next_stage_group,
-                                               start=world.has_next_stage, **kw)
-        self.backward_send_thread = SendThread(shape, group=world.prev_stage_group,
-                                               start=world.has_prev_stage, **kw)
-        self.forward_recv_thread = RecvThread(shape, group=world.prev_stage_group,
-                                              start=world.has_prev_stage, **kw)
+        self.transport = transport or os.environ.get("DILOCO_P2P_TRANSPORT", "host")
+        if self.transport == "host":
+            self.forward_send_thread = SendThread(shape, group=world.next_stage_group,
+                                                  start=world.has_next_stage, **kw)
+            self.backward_recv_thread = RecvThread(shape, group=world.next_stage_group,
+                                                   start=world.has_next_stage, **kw)
+            self.backward_send_thread = SendThread(shape, group=world.prev_stage_group,
+                                                   start=world.has_prev_stage, **kw)
+            self.forward_recv_thread = RecvThread(shape, group=world.prev_stage_group,
+                                                  start=world.has_prev_stage, **kw)
+        elif self.transport == "device":
+            from .p2p import DeviceRecvThread, DeviceSendThread, boundary_data_groups
+
+            if device is None:
+                device = torch.device("cuda", torch.cuda.current_device())
+            if serializer_factory is not None:
+                kw["serializer"] = serializer_factory(shape)
+            dg = self.data_groups = boundary_data_groups(world)
+            s = world.stage
+            nxt = (s, s + 1)
+            prv = (s - 1, s)
+            self.forward_send_thread = DeviceSendThread(
+                shape, world.next_stage_group, dg.get(nxt + ("fwd",)), device,
+                start=world.has_next_stage, **kw)
+            self.backward_recv_thread = DeviceRecvThread(
+                shape, world.next_stage_group, dg.get(nxt + ("bwd",)), device,
+                start=world.has_next_stage, **kw)
+            self.backward_send_thread = DeviceSendThread(
+                shape, world.prev_stage_group, dg.get(prv + ("bwd",)), device,
+                start=world.has_prev_stage, **kw)
+            self.forward_recv_thread = DeviceRecvThread(
+                shape, world.prev_stage_group, dg.get(prv + ("fwd",)), device,
+                start=world.has_prev_stage, **kw)
+        else:
+            raise ValueError(f"transport {self.transport!r}: 'host' or 'device'")
         self.dp = DPSync(world)
 
     # ---- pipeline p2p (unchanged protocol) ----------------------------------------------

@@ -49,6 +49,7 @@ def _worker(rank, world, port, mode, num_stages, out):
         if p not in sys.path:
             sys.path.insert(0, p)
     torch.set_num_threads(1)
+    os.environ["DILOCO_P2P_BACKEND"] = "gloo"  # the device transport's data groups, on CPU
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
@@ -142,6 +143,49 @@ def _worker(rank, world, port, mode, num_stages, out):
         gs.sync()
         rec["got"] = np.concatenate([p.grad.numpy() for p in params])
         rec["ref"] = np.concatenate([r.numpy() for r in ref])
+    elif mode == "p2p_device":
+        # header over the stage gloo group + payload over a data group
+        # (gloo here: CPU); stage 0 sends forward to random stage-1 ranks (src/comm.py:91),
+        # stage 1 answers backward to the sender
+        import random
+
+        from diloco_amd.serializer import Serializer
+
+        class CpuSerializer(Serializer):  # the reference's framing, on CPU tensors
+            def serialize(self, t, m):
+                meta = torch.zeros(t.numel())
+                meta[0], meta[1] = float(m[0]), float(m[1])
+                return torch.cat([meta.view(t.shape)[None], t[None].float()])
+
+        shape = (1, 4, 8)
+        comm = TrainingComm(world_, shape, None, transport="device",
+                            device=torch.device("cpu"), serializer_factory=CpuSerializer)
+        K = 5
+        random.seed(100 + rank)
+        stage1 = world_.stage2ranks[1]
+        if world_.stage == 0:
+            for i in range(K):
+                t = torch.arange(32, dtype=torch.float32).view(shape) + 1000 * rank + i
+                comm.send_forward(t, (rank, i))
+            got = []
+            for _ in range(K):
+                src, t, meta = comm.recv_backward()
+                got.append((src, meta[0], meta[1], float(t.sum())))
+            rec["got"] = np.array(sorted(got), dtype=np.float64)
+        else:
+            # each sender draws K choices in sequence: replay them exactly
+            n_in = 0
+            for r in world_.stage2ranks[0]:
+                g = random.Random(100 + r)
+                n_in += sum(g.choice(stage1) == rank for _ in range(K))
+            seen = []
+            for _ in range(n_in):
+                src, t, meta = comm.recv_forward()
+                assert t.requires_grad and t.shape == shape
+                seen.append((src, meta[0], meta[1], float(t.sum())))
+                comm.send_backward(src, (t * 2).detach(), meta)
+            rec["seen"] = np.array(sorted(seen), dtype=np.float64).reshape(-1, 4)
+        dist.barrier()
     elif mode == "outputs":
         comm = TrainingComm(world_, (1, 1, 4), None)
         o = Outputs(step=3, tokens=100 * (rank + 1), num_micro_batches=rank, time=1.0 + rank,
@@ -210,6 +254,24 @@ def test_gradsync_equals_per_tensor_allreduce(world):
             assert rec["got"].tobytes() == rec["ref"].tobytes()
         else:
             assert normwise_ok(rec["got"], rec["ref"], 1e-6)
+
+
+def test_device_p2p_transport_protocol():
+    """Header/payload split of the device p2p transport on 4 ranks / 2 stages: every forward
+    message reaches the rank its sender drew, with its metadata and payload; every backward
+    reply returns to its sender (src is the header's rank)."""
+    recs = _run("p2p_device", 4, num_stages=2)
+    base = float(np.arange(32).sum())
+    for r in (0, 2):  # stage 0: K replies each, payload doubled
+        got = recs[r]["got"]
+        assert len(got) == 5 and set(got[:, 1]) == {r}
+        assert sorted(got[:, 2]) == [0, 1, 2, 3, 4]
+        for src, root, i, tot in got:
+            assert src in (1, 3) and tot == 2 * (base + 32 * (1000 * r + i))
+    seen = np.concatenate([recs[1]["seen"], recs[3]["seen"]])
+    assert len(seen) == 10
+    for src, root, i, tot in seen:
+        assert src == root and tot == base + 32 * (1000 * src + i)
 
 
 def test_sync_outputs_aggregates_like_reference():

@@ -11,6 +11,7 @@ import os
 import socket
 import sys
 import tempfile
+import time
 
 import numpy as np
 import pytest
@@ -188,6 +189,39 @@ def _worker(rank, world, port, mode, out):
             rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
             rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.momentum_full()))
             rec[f"inner_s{s}"] = _flat(params)
+    elif mode == "p2p":
+        # device p2p transport with HIP framing: stage 0 -> stage 1 forward,
+        # replies backward; payload staged through host memory (gloo data groups: RCCL refuses
+        # two ranks on one GPU)
+        os.environ["DILOCO_P2P_BACKEND"] = "gloo"
+        from diloco_amd.comm import TrainingComm
+        from diloco_amd.world import World
+
+        w = World.from_default_group(2)
+        shape = (2, 16, 64)
+        comm = TrainingComm(w, shape, None, transport="device", device=torch.device("cuda", 0))
+        K = 4
+        g = torch.Generator().manual_seed(5)
+        payloads = [torch.randn(shape, generator=g) for _ in range(K)]
+        if rank == 0:
+            for i, t in enumerate(payloads):
+                dt = torch.bfloat16 if i % 2 else torch.float32  # bf16 promotes to fp32
+                comm.send_forward(t.to("cuda:0", dt), (7, i))
+            back = [comm.recv_backward() for _ in range(K)]
+            rec["back_src"] = np.array([b[0] for b in back])
+            rec["back_meta"] = np.array([b[2] for b in back])
+            rec["back"] = np.stack([b[1].detach().cpu().numpy() for b in back])
+        else:
+            fwd = [comm.recv_forward() for _ in range(K)]
+            for src, t, meta in fwd:
+                assert t.is_cuda and t.requires_grad and tuple(t.shape) == shape
+                comm.send_backward(src, t.detach() * 3, meta)
+            rec["fwd_src"] = np.array([f[0] for f in fwd])
+            rec["fwd_meta"] = np.array([f[2] for f in fwd])
+            rec["fwd"] = np.stack([f[1].detach().cpu().numpy() for f in fwd])
+        rec["want"] = np.stack([(t.to(torch.bfloat16).float() if i % 2 else t).numpy()
+                                for i, t in enumerate(payloads)])
+        time.sleep(0.5)  # let the peer's last send complete before teardown
     elif mode == "dp":
         from diloco_amd.comm import TrainingComm
         from diloco_amd.world import World
@@ -229,6 +263,19 @@ def test_two_peers_on_gpu_match_reference(mode):
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
             if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
+
+
+def test_device_p2p_transport_on_gpu():
+    """HIP-framed activations through the device p2p transport, 2 ranks / 2 stages: payloads
+    (fp32 and bf16-promoted) and metadata arrive intact, replies return to the sender."""
+    r0, r1 = _run("p2p")
+    want = r1["want"]
+    assert r1["fwd_src"].tolist() == [0] * 4
+    assert r1["fwd_meta"].tolist() == [[7, i] for i in range(4)]
+    assert r1["fwd"].tobytes() == want.tobytes()
+    assert r0["back_src"].tolist() == [1] * 4
+    assert r0["back_meta"].tolist() == [[7, i] for i in range(4)]
+    assert np.array_equal(r0["back"], want * 3)
 
 
 def test_dp_sync_of_device_grads_two_peers():
