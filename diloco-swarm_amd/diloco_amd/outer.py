@@ -8,7 +8,8 @@ One `OuterSync` per DP replica (one process per GPU). It performs, for the whole
     outer_optimizer.step()    (src/train.py:267)      -> dl_unpack_sgd   g = wire/n; Nesterov SGD
     sync_inner_model          (src/utils.py:223-226)  -> (fused in dl_unpack_sgd) inner = θ
 
-With n > 1 replicas the default is the sharded variant of SURVEY §8e (shard=True): per bucket
+With n > 1 replicas and an fp32 wire the default is the sharded variant of SURVEY §8e
+(shard=True): per bucket
 reduce-scatter of the wire -> dl_shard_sgd on this peer's 1/n (θ and momentum shards, ZeRO-1
 style) -> all-gather of θ -> dl_scatter into the inner params. Same bus bytes as the
 all-reduce; HBM traffic per peer 20 + 20/n B/param instead of 36, momentum memory 4P/n.
@@ -107,7 +108,10 @@ class OuterSync:
             raise ValueError(f"wire dtype {wire_dtype}: float32, bfloat16 or int8")
         self.q8 = wire_dtype == torch.int8
         if shard is None:
-            shard = self.world_size > 1 and not self.q8
+            # fp32 wire: same bus bytes as the all-reduce, fewer HBM bytes. bf16 wire: the
+            # fp32 all-gather of θ would move 6(n-1)/n B/param against the bf16 all-reduce's
+            # 4(n-1)/n, so the replicated step stays the default there.
+            shard = self.world_size > 1 and wire_dtype == torch.float32
         if shard and self.q8:
             raise ValueError("the int8 wire has its own exchange; shard=True needs f32/bf16")
         self.sharded = bool(shard)
