@@ -270,13 +270,20 @@ class OuterSync:
         lo, hi = self.tree.bucket_ranges[bucket]
         return self.wire[lo:hi]
 
+    def _replicated_only(self, what: str) -> None:
+        if self.sharded:
+            raise RuntimeError(f"{what}: this engine runs the sharded step (shard=True); use "
+                               "step() or reduce_scatter / shard_apply / all_gather / write_inner")
+
     def all_reduce(self, bucket: int, async_op: bool = True):
         """SUM all-reduce of one wire bucket over the DP group (RCCL), a3 minus the /n."""
+        self._replicated_only("all_reduce")
         return dist.all_reduce(self.bucket_view(bucket), op=dist.ReduceOp.SUM, group=self.group,
                                async_op=async_op)
 
     def apply(self, bucket: int = ALL, write_inner: bool = True) -> None:
         """g = wire/n; Nesterov SGD on θ_outer; inner = θ_outer (a3 /n, a4, a5)."""
+        self._replicated_only("apply")
         slot = SLOT_INNER if write_inner else -1
         if self.q8:  # the slots already hold the average
             self.k.unpack_sgd_q8(self.tree, bucket, self.q8_region(bucket), self.theta, self.mom,

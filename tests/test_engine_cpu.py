@@ -1,0 +1,75 @@
+"""OuterSync's single-process behaviour on CPU, through the oracle kernel backend
+(tests/oracle_kernels.py): the sharded step's local path (one replica, no process group),
+momentum export, and the engine's argument errors. The HIP kernels themselves are covered by
+the -m gpu tests; here the orchestration is checked against the reference fixtures."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_npz
+from diloco_amd import kernels, synth
+from diloco_amd.outer import OuterSync
+from diloco_amd.trees import get_tree
+from oracle_kernels import OracleKernels
+
+
+@pytest.fixture(autouse=True)
+def _oracle_backend():
+    prev = kernels._DEFAULT
+    kernels.set_default_kernels(OracleKernels())
+    yield
+    kernels._DEFAULT = prev
+
+
+def _micro_params():
+    spec = get_tree("micro")
+    theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
+    return spec, [torch.from_numpy(v.copy()) for v in theta0]
+
+
+def _flat(ts):
+    return np.concatenate([t.reshape(-1).numpy() for t in ts])
+
+
+@pytest.mark.parametrize("shard", [False, True])
+def test_single_replica_engine_matches_reference(shard):
+    spec, params = _micro_params()
+    g = load_npz("micro_n1.npz")
+    e = OuterSync(params, world_size=1, bucket_cap_elems=4096, shard=shard, fuse_single=False)
+    assert e.sharded == shard and e.tree.n_buckets > 2
+    for s in (1, 2):
+        vals = synth.inner_tree([t.numpy().reshape(-1) for t in e.unpacked(e.theta)], s, 0)
+        for p, v in zip(params, vals):
+            p.copy_(torch.from_numpy(v).view(p.shape))
+        e.step()
+        assert _flat(e.unpacked(e.theta)).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert _flat(e.unpacked(e.momentum_full())).tobytes() == g[f"buf_s{s}"].tobytes()
+        assert _flat(params).tobytes() == g[f"theta_s{s}"].tobytes()
+
+
+def test_engine_argument_errors():
+    _, params = _micro_params()
+    with pytest.raises(ValueError, match="int8 wire has its own exchange"):
+        OuterSync(params, world_size=2, wire_dtype=torch.int8, shard=True)
+    with pytest.raises(ValueError, match="wire dtype"):
+        OuterSync(params, world_size=1, wire_dtype=torch.float16)
+    with pytest.raises(ValueError, match="Nesterov momentum requires a momentum"):
+        OuterSync(params, world_size=1, momentum=0.0, nesterov=True)
+    with pytest.raises(ValueError, match="at least one parameter"):
+        OuterSync([], world_size=1)
+    e = OuterSync(params, world_size=1, shard=True)
+    with pytest.raises(RuntimeError, match="sharded step"):
+        e.apply()
+    with pytest.raises(RuntimeError, match="sharded step"):
+        e.all_reduce(0)
+
+
+def test_automatic_variant_choice():
+    _, params = _micro_params()
+    assert OuterSync(params, world_size=4).sharded            # fp32 wire, n > 1
+    assert not OuterSync(params, world_size=4, wire_dtype=torch.bfloat16).sharded
+    assert not OuterSync(params, world_size=4, wire_dtype=torch.int8).sharded
+    assert not OuterSync(params, world_size=1).sharded
+    e = OuterSync(params, world_size=4, bucket_cap_elems=4096)
+    for lo, hi in e.tree.bucket_ranges:  # buckets split into 4 equal 64-aligned shards
+        assert lo % 256 == 0 and (hi - lo) % 256 == 0
