@@ -112,11 +112,15 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 
 // ---- the walker ----------------------------------------------------------------------------
 // Body::operator() is instantiated per (NTL, NTS) policy: non-temporal loads / stores.
+// rev: walk the range last chunk first (workgroups are dispatched in blockIdx order), so a
+// kernel that follows one which streamed the same buffers front to back starts on the bytes
+// most likely still in the Infinity Cache.
 template <class Body, bool NTL, bool NTS>
 __global__ void __launch_bounds__(kThreads)
     k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ caddr,
-           int32_t nchunk, Body body) {
-  for (int32_t c = c0 + int32_t(blockIdx.x); c < c1; c += int32_t(gridDim.x)) {
+           int32_t nchunk, int32_t rev, Body body) {
+  for (int32_t i = int32_t(blockIdx.x); i < c1 - c0; i += int32_t(gridDim.x)) {
+    const int32_t c = rev ? c1 - 1 - i : c0 + i;
     const Chunk ck = chunks[c];
     body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x));
   }
@@ -137,7 +141,7 @@ __device__ __forceinline__ void sgd1(float g, float& buf, float& th, const SgdAr
 template <class Body, bool NTL, bool NTS>
 hipError_t run_policy(const Launch& L, const Body& body, int32_t grid) {
   hipLaunchKernelGGL((k_walk<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream, L.chunks,
-                     L.c0, L.c1, L.caddr, L.nchunk, body);
+                     L.c0, L.c1, L.caddr, L.nchunk, (L.flags & DL_TUNE_REVERSE) ? 1 : 0, body);
   return hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ ALL_BUCKETS = -1
 MAX_SLOTS = 4
 Q8_SLOT_BYTES = 4160
 DL_F32, DL_BF16, DL_F16, DL_U8 = 0, 1, 2, 3
-TUNE_NT_LOADS, TUNE_NT_STORES = 1, 2
+TUNE_NT_LOADS, TUNE_NT_STORES, TUNE_REVERSE = 1, 2, 4
 TUNE_AUTO = -1
 
 _i32, _i64, _u64, _f32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
