@@ -368,6 +368,50 @@ class OuterSync:
             gather.wait()
             self.apply(b)
 
+    # ---- checkpoint / resume -----------------------------------------------------------------
+    def state_dict(self) -> dict:
+        """Outer state in parameters() order, independent of layout and world size: per-tensor
+        θ_outer and momentum (sharded: all-gathered; collective over the group) and the step
+        count (the first step creates the momentum, torch.optim.SGD's rule)."""
+        mom = self.momentum_full()
+        return {"theta": [t.clone() for t in self.unpacked(self.theta)],
+                "momentum": None if mom is None else [t.clone() for t in self.unpacked(mom)],
+                "steps": self.steps_done, "lr": self.lr, "momentum_factor": self.momentum,
+                "nesterov": self.nesterov}
+
+    def load_state_dict(self, state: dict, write_inner: bool = True) -> None:
+        """Restore a state_dict() (from any world size / bucket layout). write_inner: also set
+        the inner parameters to θ_outer, as after an outer step."""
+        th = state["theta"]
+        if len(th) != len(self.params) or any(a.numel() != p.numel()
+                                               for a, p in zip(th, self.params)):
+            raise ValueError("state_dict does not match this engine's parameter tree")
+        with torch.no_grad():
+            for dst, src in zip(self.unpacked(self.theta), th):
+                dst.copy_(src.view(dst.shape))
+            mom = state.get("momentum")
+            if self.momentum != 0 and mom is not None:
+                full = torch.zeros(self.tree.total, dtype=torch.float32, device=self.device)
+                for dst, src in zip(self.unpacked(full), mom):
+                    dst.copy_(src.view(dst.shape))
+                if self.sharded:
+                    for b in range(self.tree.n_buckets):
+                        lo, _ = self.tree.bucket_ranges[b]
+                        s = self._shard_len(b)
+                        self._shard(self.mom_shard, b).copy_(
+                            full[lo + self.rank * s:lo + (self.rank + 1) * s])
+                else:
+                    self.mom.copy_(full)
+            if self.sharded:
+                for b in range(self.tree.n_buckets):
+                    self.th_shard_view(b).copy_(self.theta_shard_of(b))
+        self.steps_done = int(state["steps"])
+        if self.steps_done > 0 and self.momentum != 0 and state.get("momentum") is None:
+            raise ValueError("state_dict after step >= 1 must carry the momentum")
+        if write_inner:
+            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+            self.k.scatter(self.tree, ALL, self.theta, SLOT_INNER)
+
     def unpacked(self, packed: torch.Tensor) -> List[torch.Tensor]:
         """Per-tensor views into a packed buffer (shapes of the inner params)."""
         out = []

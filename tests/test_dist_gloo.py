@@ -114,6 +114,28 @@ def _worker(rank, world, port, mode, num_stages, out):
             mom = eng.momentum_full()
             rec[f"buf_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(mom)])
             rec[f"inner_s{s}"] = np.concatenate([p.numpy().reshape(-1) for p in params])
+    elif mode == "engine_resume":
+        # sharded engine: step 1, state_dict (momentum all-gathered), a fresh sharded engine
+        # with another bucket layout loads it (each rank takes its own shards), step 2
+        params = [torch.from_numpy(v.copy()) for v in theta0]
+        grp, n = world_.curr_stage_group, len(world_.dp_ranks)
+        a = OuterSync(params, group=grp, world_size=n, bucket_cap_elems=4096)
+        vals = synth.inner_tree([t.numpy().reshape(-1) for t in a.unpacked(a.theta)], 1, dp_rank)
+        for p, v in zip(params, vals):
+            p.copy_(torch.from_numpy(v))
+        a.step()
+        st = a.state_dict()
+        params2 = [torch.from_numpy(v.copy()) for v in theta0]
+        b = OuterSync(params2, group=grp, world_size=n, bucket_cap_elems=12288)
+        assert b.sharded and b.tree.n_buckets != a.tree.n_buckets
+        b.load_state_dict(st)
+        vals = synth.inner_tree([t.numpy().reshape(-1) for t in b.unpacked(b.theta)], 2, dp_rank)
+        for p, v in zip(params2, vals):
+            p.copy_(torch.from_numpy(v))
+        b.step()
+        rec["theta_s2"] = np.concatenate([t.numpy().reshape(-1) for t in b.unpacked(b.theta)])
+        rec["buf_s2"] = np.concatenate([t.numpy().reshape(-1)
+                                        for t in b.unpacked(b.momentum_full())])
     elif mode == "engine_q8":
         params = [torch.from_numpy(v.copy()) for v in theta0]
         eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=torch.int8,
@@ -233,6 +255,13 @@ def test_four_peers_match_reference_normwise(mode):
                     assert normwise_ok(a, b, 1e-6), (mode, k, s)
     for s in (1, 2):  # every replica holds the same averaged state
         assert all(r[f"theta_s{s}"].tobytes() == recs[0][f"theta_s{s}"].tobytes() for r in recs)
+
+
+def test_sharded_engine_checkpoint_resume_two_peers():
+    g = load_npz("micro_n2.npz")
+    for rec in _run("engine_resume", 2):
+        assert rec["theta_s2"].tobytes() == g["theta_s2"].tobytes()
+        assert rec["buf_s2"].tobytes() == g["buf_s2"].tobytes()
 
 
 def test_two_stages_reduce_within_their_dp_groups():

@@ -73,3 +73,39 @@ def test_automatic_variant_choice():
     e = OuterSync(params, world_size=4, bucket_cap_elems=4096)
     for lo, hi in e.tree.bucket_ranges:  # buckets split into 4 equal 64-aligned shards
         assert lo % 256 == 0 and (hi - lo) % 256 == 0
+
+
+@pytest.mark.parametrize("src_shard,dst_shard", [(False, True), (True, False), (True, True)])
+def test_checkpoint_resume_across_variants(src_shard, dst_shard):
+    """state_dict after step 1 of one engine, loaded into a fresh engine of another variant /
+    bucket layout: step 2 from the restored state equals the reference's step 2."""
+    spec, params = _micro_params()
+    g = load_npz("micro_n1.npz")
+    a = OuterSync(params, world_size=1, bucket_cap_elems=4096, shard=src_shard,
+                  fuse_single=False)
+    vals = synth.inner_tree([t.numpy().reshape(-1) for t in a.unpacked(a.theta)], 1, 0)
+    for p, v in zip(params, vals):
+        p.copy_(torch.from_numpy(v).view(p.shape))
+    a.step()
+    st = a.state_dict()
+    assert st["steps"] == 1 and len(st["momentum"]) == len(params)
+    _, params2 = _micro_params()
+    b = OuterSync(params2, world_size=1, bucket_cap_elems=8192, shard=dst_shard,
+                  fuse_single=False)
+    b.load_state_dict(st)
+    assert _flat(params2).tobytes() == g["theta_s1"].tobytes()  # inner = θ_1
+    vals = synth.inner_tree([t.numpy().reshape(-1) for t in b.unpacked(b.theta)], 2, 0)
+    for p, v in zip(params2, vals):
+        p.copy_(torch.from_numpy(v).view(p.shape))
+    b.step()
+    assert _flat(b.unpacked(b.theta)).tobytes() == g["theta_s2"].tobytes()
+    assert _flat(b.unpacked(b.momentum_full())).tobytes() == g["buf_s2"].tobytes()
+
+
+def test_load_state_dict_rejects_other_trees():
+    _, params = _micro_params()
+    e = OuterSync(params, world_size=1)
+    st = e.state_dict()
+    st["theta"] = st["theta"][:-1]
+    with pytest.raises(ValueError, match="does not match"):
+        e.load_state_dict(st)

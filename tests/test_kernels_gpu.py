@@ -578,3 +578,55 @@ def test_sharded_bf16_wire_equals_replicated_bf16_wire():
         for e, inner in zip(sh, sh_in):
             assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == want.tobytes(), s
             assert np.concatenate(_host(inner)).tobytes() == want.tobytes(), s
+
+
+def test_sharded_t125_full_size_equals_replicated():
+    """Full T125 tree (148 tensors, 2 buckets), n = 2 emulated on one GPU, 2 outer steps: the
+    sharded step (bucket-aligned layout, shard SGD, all-gather, scatter) equals the replicated
+    step bit-exact for θ, momentum and the inner parameters."""
+    spec = get_tree("t125")
+    n = 2
+    rep, rep_in = _engines(spec, n, cap=64 << 20)
+    theta0 = synth.outer_tree_device(spec, DEV)
+    shapes = [s for _, s in spec.params()]
+    sh, sh_in = [], []
+    for r in range(n):
+        inner = [t.clone().view(s) for t, s in zip(theta0, shapes)]
+        sh.append(OuterSync(inner, world_size=n, shard=True, rank=r))
+        sh_in.append(inner)
+    del theta0
+    e0 = sh[0]
+    for s in (1, 2):
+        _emulated_step(rep, rep_in, s, per_bucket=True)
+        for r, (e, inner) in enumerate(zip(sh, sh_in)):
+            th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+            synth.inner_tree_device(th, s, r, out=[p.view(-1) for p in inner])
+        for b in range(e0.tree.n_buckets):
+            for e in sh:
+                e.pseudo_gradient(b)
+            total = sh[0].bucket_view(b) + sh[1].bucket_view(b)
+            sl = e0._shard_len(b)
+            for r, e in enumerate(sh):
+                e._shard(e.g_shard, b).copy_(total[r * sl:(r + 1) * sl])
+                e.shard_apply(b)
+            gathered = torch.cat([e.th_shard_view(b) for e in sh])
+            lo, hi = e0.tree.bucket_ranges[b]
+            for e in sh:
+                e.theta[lo:hi].copy_(gathered)
+                e.write_inner(b)
+            del total, gathered
+        for e in sh:
+            e.steps_done += 1
+        torch.cuda.synchronize()
+        for a, b in zip(rep[0].unpacked(rep[0].theta), e0.unpacked(e0.theta)):
+            assert torch.equal(a, b), s
+        mom = torch.zeros_like(e0.theta)
+        for b in range(e0.tree.n_buckets):
+            lo, hi = e0.tree.bucket_ranges[b]
+            mom[lo:hi] = torch.cat([e._shard(e.mom_shard, b) for e in sh])
+        for a, b in zip(rep[0].unpacked(rep[0].mom), e0.unpacked(mom)):
+            assert torch.equal(a, b), s
+        for x, y in zip(rep_in[1], sh_in[1]):
+            assert torch.equal(x, y), s
+    for e in rep + sh:
+        e.close()
