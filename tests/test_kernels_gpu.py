@@ -630,3 +630,41 @@ def test_sharded_t125_full_size_equals_replicated():
             assert torch.equal(x, y), s
     for e in rep + sh:
         e.close()
+
+
+def test_tensor_larger_than_int32_elements():
+    """A tensor of 2^31 + 5 elements (8.6 GB; 64-bit offsets in the planner, chunk table and
+    kernels) between two small ones: one outer step through the two-kernel path and the fused
+    path agree bit-exact, and elements around the 2^31 boundary and at the end equal the
+    oracle's step computed on the host."""
+    big = (1 << 31) + 5
+    numels = [3, big, 7]
+    n_total = sum(numels)
+    free, _ = torch.cuda.mem_get_info()
+    if free < 12 * 4 * n_total:
+        pytest.skip("needs ~100 GB of free HBM")
+    params = [torch.empty(n, device=DEV) for n in numels]
+    for i, p in enumerate(params):
+        synth.fill_device(p, 42, i, 0.0, 0.02)
+    pb = [p.clone() for p in params]
+    ea = OuterSync(params, world_size=1, fuse_single=False)
+    eb = OuterSync(pb, world_size=1, fuse_single=True)
+    assert ea.tree.seg_off[-1] > (1 << 31)
+    for e, ps in ((ea, params), (eb, pb)):
+        for i, p in enumerate(ps):  # inner = θ_0 + noise
+            synth.fill_device(p, 7, i, 0.0, 1e-3, add=e.unpacked(e.theta)[i])
+        e.step()
+    torch.cuda.synchronize()
+    for x, y in zip(params, pb):
+        assert torch.equal(x, y)
+    del pb, eb
+    # host check of slices of the big tensor (SGD first step: θ1 = θ0 - lr*(1+m)*(θ0 - inner))
+    for lo in (0, (1 << 31) - 8, big - 9):
+        n = 9 if lo == big - 9 else 16
+        th0 = np.float32(0.0) + synth.uniform(42, 1, n, start=lo) * np.float32(0.02)
+        inner = (np.float32(0.0) + synth.uniform(7, 1, n, start=lo) * np.float32(1e-3)) + th0
+        st = oracle.OuterState([th0])
+        st.step([[inner]])
+        got = params[1][lo:lo + n].cpu().numpy()
+        assert got.tobytes() == st.theta[0].tobytes(), lo
+    ea.close()
