@@ -659,12 +659,11 @@ def test_tensor_larger_than_int32_elements():
         assert torch.equal(x, y)
     del pb, eb
     # host check of slices of the big tensor (SGD first step: θ1 = θ0 - lr*(1+m)*(θ0 - inner))
-    for lo in (0, (1 << 31) - 8, big - 9):
-        n = 9 if lo == big - 9 else 16
+    for lo, n in ((0, 16), ((1 << 31) - 8, 13), (big - 9, 9)):  # 13: up to the last element
         th0 = np.float32(0.0) + synth.uniform(42, 1, n, start=lo) * np.float32(0.02)
         inner = (np.float32(0.0) + synth.uniform(7, 1, n, start=lo) * np.float32(1e-3)) + th0
         st = oracle.OuterState([th0])
         st.step([[inner]])
         got = params[1][lo:lo + n].cpu().numpy()
-        assert got.tobytes() == st.theta[0].tobytes(), lo
+        assert got.size == n and got.tobytes() == st.theta[0].tobytes(), lo
     ea.close()
