@@ -417,6 +417,73 @@ DL_API int dl_shard_sgd(const void* wire, int32_t wire_dtype, int32_t divisor, f
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_shard_sgd");
 }
 
+DL_API int dl_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
+  if (!ptr || !handle || !offset) return fail(DL_E_ARG, "dl_ipc_handle: null argument");
+  void* base = nullptr;
+  size_t size = 0;
+  DL_HIP(hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)), "dl_ipc_handle");
+  hipIpcMemHandle_t h;
+  DL_HIP(hipIpcGetMemHandle(&h, base), "dl_ipc_handle");
+  static_assert(sizeof(h) <= DL_IPC_HANDLE_BYTES, "IPC handle size");
+  std::memset(handle, 0, DL_IPC_HANDLE_BYTES);
+  std::memcpy(handle, &h, sizeof h);
+  *offset = static_cast<const char*>(ptr) - static_cast<const char*>(base);
+  return DL_OK;
+}
+
+DL_API int dl_ipc_open(const void* handle, void** base) {
+  if (!handle || !base) return fail(DL_E_ARG, "dl_ipc_open: null argument");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof h);
+  DL_HIP(hipIpcOpenMemHandle(base, h, hipIpcMemLazyEnablePeerAccess), "dl_ipc_open");
+  return DL_OK;
+}
+
+DL_API int dl_ipc_close(void* base) {
+  if (!base) return DL_OK;
+  DL_HIP(hipIpcCloseMemHandle(base), "dl_ipc_close");
+  return DL_OK;
+}
+
+DL_API int dl_can_access_peer(int32_t device, int32_t peer, int32_t* can) {
+  if (!can) return fail(DL_E_ARG, "dl_can_access_peer: null argument");
+  if (device == peer) {
+    *can = 1;
+    return DL_OK;
+  }
+  int c = 0;
+  DL_HIP(hipDeviceCanAccessPeer(&c, device, peer), "dl_can_access_peer");
+  *can = c;
+  return DL_OK;
+}
+
+DL_API int dl_xgmi_reduce_sgd(const uint64_t* wires, const uint64_t* thetas, int32_t n,
+                              int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
+                              float momentum, int32_t nesterov, int32_t first_step,
+                              dl_stream_t s) {
+  if (!wires || !thetas) return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: null peer table");
+  if (n < 1 || n > dl::kMaxPeers || rank < 0 || rank >= n)
+    return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: rank %d of %d (1..%d peers)", rank, n,
+                dl::kMaxPeers);
+  if (lo < 0 || len < 0 || lo % 4 || len % 4)
+    return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: shard [%lld, +%lld) not a multiple of 4",
+                (long long)lo, (long long)len);
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_xgmi_reduce_sgd", "momentum"));
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: Nesterov momentum requires a momentum");
+  dl::XgmiPeers p{};
+  for (int32_t q = 0; q < n; ++q) {
+    p.wire[q] = reinterpret_cast<const float*>(wires[q]);
+    p.theta[q] = reinterpret_cast<float*>(thetas[q]);
+    DL_TRY(check_packed(p.wire[q], "dl_xgmi_reduce_sgd", "wire"));
+    DL_TRY(check_packed(p.theta[q], "dl_xgmi_reduce_sgd", "theta"));
+  }
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_xgmi_reduce_sgd(p, n, rank, lo, len, mom, a,
+                                            static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_xgmi_reduce_sgd");
+}
+
 DL_API int dl_delta_q8(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,
                        void* slots, dl_stream_t s) {
   dl::Launch L;

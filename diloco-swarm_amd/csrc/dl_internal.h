@@ -41,6 +41,15 @@ struct Launch {
   hipStream_t stream;
 };
 
+// peers of the direct exchange (dl_xgmi.hip): each rank's packed wire and θ, IPC-mapped
+constexpr int kMaxPeers = 8;
+struct XgmiPeers {
+  const float* wire[kMaxPeers];
+  float* theta[kMaxPeers];
+};
+hipError_t launch_xgmi_reduce_sgd(const XgmiPeers& p, int32_t n, int32_t rank, int64_t lo,
+                                  int64_t len, float* mom, SgdArgs a, hipStream_t s);
+
 // dl_last_error() text for entry points outside dl_abi.hip; returns `code`
 int set_error(int code, const char* msg);
 

@@ -1,0 +1,102 @@
+// Direct peer-access exchange for the outer step (an alternative to RCCL's
+// reduce-scatter + all-gather on one node): every rank's packed wire and θ_outer buffers are
+// IPC-mapped into every peer, and ONE kernel per rank does, for its 1/n shard of the packed
+// tree,
+//     g = ((wire_0 + wire_1) + ... + wire_{n-1}) / n     rank order: identical on every rank,
+//                                                        bit-exact vs oracle/or_sum_avg
+//     Nesterov SGD on θ_rank and the momentum shard      (dl_unpack_sgd's arithmetic)
+//     θ_q[k] = θ_new for every peer q                    (the all-gather, as remote stores)
+// so the exchange crosses xGMI once per direction per byte, with no staging buffers. The
+// caller orders it between two collective barriers (all wires written before any peer reads;
+// all θ stores landed before any rank reads θ again); nothing in the kernel waits on a peer.
+#include "dl_device.h"
+
+namespace dl {
+namespace {
+
+constexpr int kXU = 2;                          // float4 per lane per stream
+constexpr int kXChunk = kThreads * kXU * 4;     // 2048 elements per workgroup
+
+template <int N>
+__global__ void __launch_bounds__(kThreads)
+    k_xgmi_reduce_sgd(XgmiPeers p, int32_t rank, int64_t lo, int64_t len, float* __restrict__ mom,
+                      SgdArgs a, int32_t mode) {
+  for (int64_t base = int64_t(blockIdx.x) * kXChunk; base < len;
+       base += int64_t(gridDim.x) * kXChunk) {
+    float4 w[N][kXU];
+    float4 t[kXU], m[kXU];
+    const int64_t k0 = lo + base;  // packed index of this workgroup's first element
+#pragma unroll
+    for (int u = 0; u < kXU; ++u) {
+      const int64_t e = base + int64_t(u * kThreads + threadIdx.x) * 4;
+      if (e < len) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) w[q][u] = ldf4<true>(p.wire[q] + k0, u * kThreads + threadIdx.x);
+        t[u] = ldf4<true>(p.theta[rank] + k0, u * kThreads + threadIdx.x);
+        if (mode == 2) m[u] = ldf4<true>(mom + base, u * kThreads + threadIdx.x);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kXU; ++u) {
+      const int64_t e = base + int64_t(u * kThreads + threadIdx.x) * 4;
+      if (e < len) {
+        float4 g = w[0][u];
+#pragma unroll
+        for (int q = 1; q < N; ++q)
+          g = make_float4(g.x + w[q][u].x, g.y + w[q][u].y, g.z + w[q][u].z, g.w + w[q][u].w);
+        if (N > 1) g = div4(g, float(N));
+        if (mode == 0) {
+          sgd1<0>(g.x, m[u].x, t[u].x, a);
+          sgd1<0>(g.y, m[u].y, t[u].y, a);
+          sgd1<0>(g.z, m[u].z, t[u].z, a);
+          sgd1<0>(g.w, m[u].w, t[u].w, a);
+        } else if (mode == 1) {
+          sgd1<1>(g.x, m[u].x, t[u].x, a);
+          sgd1<1>(g.y, m[u].y, t[u].y, a);
+          sgd1<1>(g.z, m[u].z, t[u].z, a);
+          sgd1<1>(g.w, m[u].w, t[u].w, a);
+        } else {
+          sgd1<2>(g.x, m[u].x, t[u].x, a);
+          sgd1<2>(g.y, m[u].y, t[u].y, a);
+          sgd1<2>(g.z, m[u].z, t[u].z, a);
+          sgd1<2>(g.w, m[u].w, t[u].w, a);
+        }
+        if (mode != 0) stf4<true>(mom + base, u * kThreads + threadIdx.x, m[u]);
+#pragma unroll
+        for (int q = 0; q < N; ++q) stf4<true>(p.theta[q] + k0, u * kThreads + threadIdx.x, t[u]);
+      }
+    }
+  }
+  __threadfence_system();  // remote θ stores ordered before the kernel's completion
+}
+
+template <int N>
+hipError_t launch_n(const XgmiPeers& p, int32_t rank, int64_t lo, int64_t len, float* mom,
+                    SgdArgs a, hipStream_t s) {
+  const int32_t mode = a.momentum == 0.f ? 0 : (a.first ? 1 : 2);
+  const int64_t blocks = (len + kXChunk - 1) / kXChunk;
+  const int32_t grid = int32_t(blocks < 65536 ? blocks : 65536);
+  hipLaunchKernelGGL(k_xgmi_reduce_sgd<N>, dim3(grid), dim3(kThreads), 0, s, p, rank, lo, len, mom,
+                     a, mode);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_xgmi_reduce_sgd(const XgmiPeers& p, int32_t n, int32_t rank, int64_t lo,
+                                  int64_t len, float* mom, SgdArgs a, hipStream_t s) {
+  if (len <= 0) return hipSuccess;
+  switch (n) {
+    case 1: return launch_n<1>(p, rank, lo, len, mom, a, s);
+    case 2: return launch_n<2>(p, rank, lo, len, mom, a, s);
+    case 3: return launch_n<3>(p, rank, lo, len, mom, a, s);
+    case 4: return launch_n<4>(p, rank, lo, len, mom, a, s);
+    case 5: return launch_n<5>(p, rank, lo, len, mom, a, s);
+    case 6: return launch_n<6>(p, rank, lo, len, mom, a, s);
+    case 7: return launch_n<7>(p, rank, lo, len, mom, a, s);
+    case 8: return launch_n<8>(p, rank, lo, len, mom, a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace dl

@@ -21,6 +21,7 @@ CHUNK_ELEMS = 4096
 ALL_BUCKETS = -1
 MAX_SLOTS = 4
 Q8_SLOT_BYTES = 4160
+IPC_HANDLE_BYTES = 64
 DL_F32, DL_BF16, DL_F16, DL_U8 = 0, 1, 2, 3
 TUNE_NT_LOADS, TUNE_NT_STORES, TUNE_REVERSE = 1, 2, 4
 TUNE_AUTO = -1
@@ -71,6 +72,14 @@ SIGNATURES = {
     "dl_allreduce": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "dl_reduce_scatter": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "dl_all_gather": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "dl_ipc_handle": (ctypes.c_int, [_vp, _vp, _pi64]),
+    "dl_ipc_open": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "dl_ipc_close": (ctypes.c_int, [_vp]),
+    "dl_can_access_peer": (ctypes.c_int, [_i32, _i32, _pi32]),
+    "dl_xgmi_reduce_sgd": (
+        ctypes.c_int,
+        [_pu64, _pu64, _i32, _i32, _i64, _i64, _vp, _f32, _f32, _i32, _i32, _vp],
+    ),
     "dl_last_error": (ctypes.c_char_p, []),
     "dl_abi_version": (ctypes.c_int, []),
 }

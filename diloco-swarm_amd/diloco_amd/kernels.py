@@ -7,6 +7,8 @@ HIP stream of the tensors' device and raises if the library or the GPU is missin
 """
 from __future__ import annotations
 
+import ctypes
+
 from typing import Optional, Sequence
 
 import torch
@@ -75,6 +77,16 @@ class HipKernels:
         _lib.call("dl_shard_sgd", wire.data_ptr(), wire_code(wire.dtype), int(divisor),
                   theta.data_ptr(), _ptr(mom), theta.numel(), float(lr), float(momentum),
                   int(nesterov), int(first), _s(theta))
+
+    def xgmi_reduce_sgd(self, wires, thetas, n, rank, lo, length, mom, lr, momentum, nesterov,
+                        first, device=None) -> None:
+        """Direct exchange on this rank's shard (wires / thetas: uint64 arrays of the n peers'
+        device addresses, IPC-mapped)."""
+        p64 = ctypes.POINTER(ctypes.c_uint64)
+        _lib.call("dl_xgmi_reduce_sgd", wires.ctypes.data_as(p64), thetas.ctypes.data_as(p64),
+                  int(n), int(rank), int(lo), int(length), _ptr(mom), float(lr),
+                  float(momentum), int(nesterov), int(first),
+                  torch.cuda.current_stream(device).cuda_stream)
 
     # int8 wire codec (DL_Q8_SLOT_BYTES slots, one per chunk)
     def delta_q8(self, tree, bucket, inner_slot, theta, slots) -> None:

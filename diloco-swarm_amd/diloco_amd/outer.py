@@ -84,6 +84,7 @@ class OuterSync:
         side_stream: bool = True,
         shard: Optional[bool] = None,
         rank: Optional[int] = None,
+        exchange: str = "rccl",
     ):
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
                                            for p in params]
@@ -114,9 +115,15 @@ class OuterSync:
             shard = self.world_size > 1 and wire_dtype == torch.float32
         if shard and self.q8:
             raise ValueError("the int8 wire has its own exchange; shard=True needs f32/bf16")
-        self.sharded = bool(shard)
-        # sharded: every bucket starts at a multiple of 64·n elements -> n equal aligned shards
-        balign = _lib.ALIGN_ELEMS * (self.world_size if self.sharded else 1)
+        if exchange not in ("rccl", "xgmi"):
+            raise ValueError(f"exchange {exchange!r}: 'rccl' or 'xgmi'")
+        # xgmi: the direct peer-access exchange (dl_xgmi_reduce_sgd) over IPC-mapped buffers
+        self.xgmi = exchange == "xgmi"
+        if self.xgmi and wire_dtype != torch.float32:
+            raise ValueError("exchange='xgmi' sends the fp32 wire")
+        self.sharded = bool(shard) and not self.xgmi
+        # sharded / xgmi: buckets (and the tree) align to 64·n elements -> n equal aligned shards
+        balign = _lib.ALIGN_ELEMS * (self.world_size if (self.sharded or self.xgmi) else 1)
         self.tree = self.k.tree([p.numel() for p in self.params], self.device, bucket_cap_elems,
                                 balign)
         self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
@@ -125,7 +132,7 @@ class OuterSync:
         z = dict(device=self.device)
         self.theta = torch.zeros(self.tree.total, dtype=torch.float32, **z)
         self.mom = (torch.zeros(self.tree.total, dtype=torch.float32, **z)
-                    if self.momentum != 0 and not self.sharded else None)
+                    if self.momentum != 0 and not (self.sharded or self.xgmi) else None)
         if self.q8:
             # int8 codec: one Q8_SLOT-byte slot per chunk; bucket b's slots padded to a
             # multiple of the peer count so both exchanges split evenly (dl_q8.hip)
@@ -159,6 +166,19 @@ class OuterSync:
             self.g_shard = torch.zeros(off, dtype=wire_dtype, **z)
             self.mom_shard = (torch.zeros(off, dtype=torch.float32, **z)
                               if self.momentum != 0 else None)
+        if self.xgmi:
+            from .xgmi import PeerMap
+
+            n = self.world_size
+            self.x_len = self.tree.total // n
+            self.x_lo = self.rank * self.x_len
+            self.mom_x = (torch.zeros(self.x_len, dtype=torch.float32, **z)
+                          if self.momentum != 0 else None)
+            self._flag = torch.zeros(1, dtype=torch.float32, **z)
+            self.peers = PeerMap({"wire": self.wire, "theta": self.theta},
+                                 group if n > 1 else None, self.device)
+            if not self.peers.ok:
+                raise RuntimeError(f"exchange='xgmi' unavailable: {self.peers.reason}")
         self.steps_done = 0
         # step() runs on its own stream, ordered after the caller's current stream and joined
         # back into it: work other threads put on the default stream meanwhile (the
@@ -252,6 +272,15 @@ class OuterSync:
 
     def momentum_full(self) -> Optional[torch.Tensor]:
         """The packed momentum of the whole tree (sharded: all-gathered; for checks/export)."""
+        if self.xgmi:
+            if self.mom_x is None:
+                return None
+            out = torch.empty(self.tree.total, dtype=torch.float32, device=self.device)
+            if self.world_size > 1:
+                dist.all_gather_into_tensor(out, self.mom_x, group=self.group)
+            else:
+                out.copy_(self.mom_x)
+            return out
         if not self.sharded or self.mom_shard is None:
             return self.mom
         out = torch.zeros(self.tree.total, dtype=torch.float32, device=self.device)
@@ -271,6 +300,9 @@ class OuterSync:
         return self.wire[lo:hi]
 
     def _replicated_only(self, what: str) -> None:
+        if self.xgmi:
+            raise RuntimeError(f"{what}: this engine exchanges through IPC (exchange='xgmi'); "
+                               "use step()")
         if self.sharded:
             raise RuntimeError(f"{what}: this engine runs the sharded step (shard=True); use "
                                "step() or reduce_scatter / shard_apply / all_gather / write_inner")
@@ -313,6 +345,8 @@ class OuterSync:
             pipeline = self.world_size > 1
         if self.q8:
             self._step_q8(pipeline)
+        elif self.xgmi:
+            self._step_xgmi()
         elif self.sharded:
             self._step_sharded()
         elif pipeline:
@@ -348,6 +382,25 @@ class OuterSync:
                 self.write_inner(b - 1)
         ag[nb - 1].wait()
         self.write_inner(nb - 1)
+
+    def _barrier(self) -> None:
+        """All ranks' preceding work on their streams is complete (a stream-ordered 4-B
+        all-reduce with RCCL; gloo blocks the host)."""
+        if self.world_size > 1:
+            dist.all_reduce(self._flag, group=self.group)
+
+    def _step_xgmi(self) -> None:
+        """delta_pack -> barrier -> dl_xgmi_reduce_sgd (peers' wires summed in rank order, SGD
+        on this rank's shard, θ shard stored into every peer) -> barrier -> inner = θ."""
+        self.pseudo_gradient(ALL)
+        self._barrier()
+        self.k.xgmi_reduce_sgd(self.peers.table("wire"), self.peers.table("theta"),
+                               self.world_size, self.rank, self.x_lo, self.x_len, self.mom_x,
+                               self.lr, self.momentum, self.nesterov, self.steps_done == 0,
+                               self.device)
+        self._barrier()
+        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+        self.k.scatter(self.tree, ALL, self.theta, SLOT_INNER)
 
     def _step_q8(self, pipeline: bool) -> None:
         nb = self.tree.n_buckets
@@ -394,7 +447,9 @@ class OuterSync:
                 full = torch.zeros(self.tree.total, dtype=torch.float32, device=self.device)
                 for dst, src in zip(self.unpacked(full), mom):
                     dst.copy_(src.view(dst.shape))
-                if self.sharded:
+                if self.xgmi:
+                    self.mom_x.copy_(full[self.x_lo:self.x_lo + self.x_len])
+                elif self.sharded:
                     for b in range(self.tree.n_buckets):
                         lo, _ = self.tree.bucket_ranges[b]
                         s = self._shard_len(b)
@@ -421,4 +476,7 @@ class OuterSync:
         return out
 
     def close(self) -> None:
+        if getattr(self, "peers", None) is not None:
+            self.peers.close()
+            self.peers = None
         self.tree.close()

@@ -189,6 +189,27 @@ def _worker(rank, world, port, mode, out):
             rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
             rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.momentum_full()))
             rec[f"inner_s{s}"] = _flat(params)
+    elif mode == "engine_xgmi":
+        # the direct exchange: wires and θ IPC-mapped between the processes (same GPU here),
+        # one dl_xgmi_reduce_sgd per rank between two barriers
+        from diloco_amd import synth
+        from diloco_amd.outer import OuterSync
+        from diloco_amd.trees import get_tree
+
+        spec = get_tree("micro")
+        shapes = [s for _, s in spec.params()]
+        params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+        eng = OuterSync(params, world_size=world, bucket_cap_elems=4096, exchange="xgmi")
+        assert eng.xgmi and eng.tree.total % (64 * world) == 0
+        for s in (1, 2):
+            th = [t.reshape(-1) for t in eng.unpacked(eng.theta)]
+            synth.inner_tree_device(th, s, rank, out=[p.view(-1) for p in params])
+            eng.step()
+            torch.cuda.synchronize()
+            rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
+            rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.momentum_full()))
+            rec[f"inner_s{s}"] = _flat(params)
+        eng.close()
     elif mode == "p2p":
         # device p2p transport with HIP framing: stage 0 -> stage 1 forward,
         # replies backward; payload staged through host memory (gloo data groups: RCCL refuses
@@ -247,7 +268,7 @@ def _worker(rank, world, port, mode, out):
     dist.destroy_process_group()
 
 
-def _run(mode, world=2):
+def _run(mode, world=2):  # noqa: D401
     out = tempfile.mkdtemp(prefix="dl_gpu_")
     mp.spawn(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True)
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
@@ -263,6 +284,30 @@ def test_two_peers_on_gpu_match_reference(mode):
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
             if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_direct_exchange_between_processes(world):
+    """exchange='xgmi' with `world` processes on the one GPU (IPC between processes of one
+    device; across devices the same code reads over xGMI): every replica equals the oracle's
+    rank-order sum + SGD bit-exact at any n, and the reference bit-exact at n = 2."""
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from oracle import oracle
+
+    recs = _run("engine_xgmi", world)
+    spec = get_tree("micro")
+    st = oracle.OuterState(synth.outer_tree(spec.numels(), spec.init_spec()))
+    for s in (1, 2):
+        st.step([synth.inner_tree(st.theta, s, r) for r in range(world)])
+        want_th = np.concatenate(st.theta)
+        want_buf = np.concatenate(st.buf)
+        for rec in recs:
+            assert rec[f"theta_s{s}"].tobytes() == want_th.tobytes(), s
+            assert rec[f"buf_s{s}"].tobytes() == want_buf.tobytes(), s
+            assert rec[f"inner_s{s}"].tobytes() == want_th.tobytes(), s
+        if world == 2:
+            assert want_th.tobytes() == load_npz("micro_n2.npz")[f"theta_s{s}"].tobytes()
 
 
 def test_device_p2p_transport_on_gpu():
