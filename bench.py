@@ -76,12 +76,12 @@ def setup_dist(n_gpus):
     return ws, rank, dev
 
 
-def build(spec, dev, rank, wire, cap, fuse=False, shard=None):
+def build(spec, dev, rank, wire, cap, fuse=False, shard=None, exchange="rccl"):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree_device(spec, dev)
     params = [t.view(s) for t, s in zip(theta0, shapes)]
     eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=wire,
-                    bucket_cap_elems=cap, fuse_single=fuse, shard=shard)
+                    bucket_cap_elems=cap, fuse_single=fuse, shard=shard, exchange=exchange)
     # inner = θ_0 + this rank's noise (stands in for H inner steps)
     synth.inner_tree_device([p.view(-1) for p in params], 1, rank, out=[p.view(-1) for p in params])
     return eng
@@ -110,11 +110,11 @@ def kernel_entry(bytes_per_launch, ms, traffic=None, bound="hbm", peak=HBM_PEAK_
 
 
 def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loops=True,
-             shard=None):
+             shard=None, exchange="rccl"):
     """Timed region (K outer steps, nothing else on the stream), then an instrumented pass of
     K more steps with HIP events between the kernels on the stream they run on (events in the
     timed region would cost the step ~35 us each), then the same kernels back to back."""
-    eng = build(spec, dev, rank, wire, cap, fuse, shard)
+    eng = build(spec, dev, rank, wire, cap, fuse, shard, exchange)
     P = spec.total()
     for _ in range(max(warmup, 1)):  # >= 1: the timed steps run the steady-state SGD mode
         eng.step()
@@ -150,7 +150,8 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
            "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
            "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * P / (dt / steps) / 1e9,
            "wire": "bf16" if wire == torch.bfloat16 else "f32",
-           "variant": ("reduce_scatter -> shard SGD -> all_gather" if eng.sharded
+           "variant": ("direct peer-access exchange (IPC, dl_xgmi_reduce_sgd)" if eng.xgmi
+                       else "reduce_scatter -> shard SGD -> all_gather" if eng.sharded
                        else "all_reduce -> replicated SGD")}
     if single and fuse:
         b = 24 * P  # read θ, inner, buf; write θ, buf, inner
@@ -174,13 +175,21 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         e1.synchronize()
         return e0.elapsed_time(e1) / reps
 
-    if b2b_loops and not eng.sharded:
+    if b2b_loops and not (eng.sharded or eng.xgmi):
         res["kernels_b2b"] = {"delta_pack": kernel_entry((8 + wb) * P, b2b(eng.pseudo_gradient)),
                               "unpack_sgd": kernel_entry((wb + 20) * P, b2b(eng.apply))}
     if single:
         ks = res["kernels"]
         dom = max(ks, key=lambda k: ks[k]["avg_ms"])
         res["roofline"] = dict(ks[dom], kernel=dom)
+    elif eng.xgmi:
+        # the exchange kernel moves (n-1)/n·4P in (peer wires) and (n-1)/n·4P out (θ stores);
+        # over the whole step time this is a lower bound on its xGMI rate
+        bus = 2.0 * (ws - 1) / ws * 4 * eng.tree.total
+        res["roofline"] = dict(kernel_entry(bus, dt / steps * 1e3, bound="xgmi",
+                                            peak=(ws - 1) * XGMI_LINK_GBS),
+                               kernel="dl_xgmi_reduce_sgd (whole step, lower bound)",
+                               bus_bytes_per_step=bus)
     else:
         def collectives_all():
             for b in range(eng.tree.n_buckets):
@@ -252,6 +261,40 @@ def parity_check(dev, ws, rank, wire):
     return {"tree": "tiny", "buckets": nb, "wire": "f32" if wire == torch.float32 else "bf16",
             "avg_delta_normwise_err": worst, "tolerance": tol,
             "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
+
+
+def parity_xgmi(dev, ws, rank):
+    """The direct exchange (exchange='xgmi') against the RCCL sharded step on the tiny tree,
+    2 outer steps: θ and momentum normwise <= 1e-6 per tensor (bit-exact at n <= 2; the direct
+    exchange sums in rank order, RCCL in its own order), inner == θ, replicas identical."""
+    spec = get_tree("tiny")
+    ea = build(spec, dev, rank, torch.float32, 1 << 20, exchange="xgmi")
+    eb = build(spec, dev, rank, torch.float32, 1 << 20)
+    for s in (1, 2):
+        for e in (ea, eb):
+            if s > 1:
+                th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+                synth.inner_tree_device(th, s, rank, out=[p.view(-1) for p in e.params])
+            e.step()
+    torch.cuda.synchronize()
+    worst, exact = 0.0, True
+    ma, mb = ea.momentum_full(), eb.momentum_full()
+    for x, y in ((ea.theta, eb.theta), (ma, mb)):
+        for a, b in zip(ea.unpacked(x), eb.unpacked(y)):
+            exact &= bool(torch.equal(a, b))
+            scale = float(b.abs().max().clamp_min(1e-30))
+            worst = max(worst, float((a - b).abs().max()) / scale)
+    inner_ok = all(torch.equal(p, t) for p, t in zip(ea.params, ea.unpacked(ea.theta)))
+    bits = ea.theta.view(torch.int32).to(torch.int64).sum()
+    ck = torch.stack([bits, -bits])
+    if ws > 1:
+        dist.all_reduce(ck, op=dist.ReduceOp.MAX)
+    identical = bool(ck[0].item() == -ck[1].item())
+    ea.close()
+    eb.close()
+    return {"tree": "tiny", "steps": 2, "xgmi_vs_rccl_normwise_err": worst, "bit_exact": exact,
+            "tolerance": 1e-6, "inner_is_theta": inner_ok, "replicas_identical": identical,
+            "ok": bool(worst <= 1e-6 and identical and inner_ok)}
 
 
 def parity_sharded(dev, ws, rank):
@@ -588,6 +631,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the host-outer-model rate")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-xgmi", action="store_true",
+                    help="skip the direct peer-access exchange legs at N > 1")
     ap.add_argument("--p2p", action="store_true",
                     help="also time the device p2p transport (N even; SURVEY §8f row 3)")
     ap.add_argument("--only-headline", action="store_true",
@@ -644,6 +689,13 @@ def main():
         if rank == 0 and ws == 1 and not a.no_cpu_baseline:
             log("timing the CPU baseline")
             cpu = cpu_baseline(spec)
+        if ws > 1 and not a.no_xgmi:
+            # last: the direct peer-access exchange (IPC-mapped wires / θ, one fused kernel)
+            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, torch.float32, cap,
+                       False, False, None, "xgmi")
+            extra[f"{spec.name}_xgmi_exchange"] = _brief(r) if "value" in r else r
+            if parity is not None:
+                parity["xgmi"] = _guard(parity_xgmi, dev, ws, rank)
     if rank == 0:
         line = {
             "metric": METRIC,

@@ -457,6 +457,15 @@ DL_API int dl_can_access_peer(int32_t device, int32_t peer, int32_t* can) {
   return DL_OK;
 }
 
+DL_API int dl_enable_peer_access(int32_t peer) {
+  hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();  // clear the sticky "already enabled"
+    return DL_OK;
+  }
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_enable_peer_access");
+}
+
 DL_API int dl_xgmi_reduce_sgd(const uint64_t* wires, const uint64_t* thetas, int32_t n,
                               int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
                               float momentum, int32_t nesterov, int32_t first_step,

@@ -76,6 +76,7 @@ SIGNATURES = {
     "dl_ipc_open": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "dl_ipc_close": (ctypes.c_int, [_vp]),
     "dl_can_access_peer": (ctypes.c_int, [_i32, _i32, _pi32]),
+    "dl_enable_peer_access": (ctypes.c_int, [_i32]),
     "dl_xgmi_reduce_sgd": (
         ctypes.c_int,
         [_pu64, _pu64, _i32, _i32, _i64, _i64, _vp, _f32, _f32, _i32, _i32, _vp],

@@ -477,6 +477,9 @@ class OuterSync:
 
     def close(self) -> None:
         if getattr(self, "peers", None) is not None:
+            if self.world_size > 1:  # nobody still reads a buffer this rank is about to unmap
+                torch.cuda.synchronize(self.device)
+                dist.barrier(group=self.group)
             self.peers.close()
             self.peers = None
         self.tree.close()

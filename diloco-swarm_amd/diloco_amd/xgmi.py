@@ -55,23 +55,39 @@ class PeerMap:
         everyone: List[dict] = [None] * self.n
         dist.all_gather_object(everyone, mine, group=group)
         if self.ok:
-            self.ok, self.reason = self._check(everyone, mine)
+            try:
+                self.ok, self.reason = self._check(everyone, mine)
+            except _lib.DilocoHipError as e:  # a failed query is a "no" vote, never a raise
+                self.ok, self.reason = False, f"peer query failed: {e}"
         votes: List[tuple] = [None] * self.n
         dist.all_gather_object(votes, (self.ok, self.reason), group=group)
         bad = [f"rank {q}: {r}" for q, (o, r) in enumerate(votes) if not o]
         if bad:
             self.ok, self.reason = False, "; ".join(bad)
             return
-        for q, info in enumerate(everyone):
-            if q == self.rank:
-                continue
-            for k in self.names:
-                handle, off = info["bufs"][k]
-                base = ctypes.c_void_p()
-                _lib.call("dl_ipc_open", ctypes.create_string_buffer(handle, len(handle)),
-                          ctypes.byref(base))
-                self._opened.append(base.value)
-                self.ptrs[k][q] = base.value + off
+        err = ""
+        try:
+            for d in sorted({info["device"] for info in everyone} - {dev}):
+                _lib.call("dl_enable_peer_access", int(d))
+            for q, info in enumerate(everyone):
+                if q == self.rank:
+                    continue
+                for k in self.names:
+                    handle, off = info["bufs"][k]
+                    base = ctypes.c_void_p()
+                    _lib.call("dl_ipc_open", ctypes.create_string_buffer(handle, len(handle)),
+                              ctypes.byref(base))
+                    self._opened.append(base.value)
+                    self.ptrs[k][q] = base.value + off
+        except _lib.DilocoHipError as e:
+            err = f"opening a peer's buffer failed: {e}"
+        # second agreement: every rank mapped every peer, or every rank gives up together
+        votes = [None] * self.n
+        dist.all_gather_object(votes, err, group=group)
+        bad = [f"rank {q}: {r}" for q, r in enumerate(votes) if r]
+        if bad:
+            self.close()
+            self.ok, self.reason = False, "; ".join(bad)
 
     def _check(self, everyone, mine):
         for q, info in enumerate(everyone):

@@ -219,7 +219,8 @@ DL_API int dl_all_gather(const void* send, void* recv, int64_t send_count, int32
 /* ---- direct peer-access exchange (one node; SURVEY §8e alternative to RCCL) ----------------
  * IPC: dl_ipc_handle(ptr) -> the handle of the allocation holding ptr + ptr's byte offset in
  * it; a peer maps it with dl_ipc_open (base address; add the offset) and unmaps with
- * dl_ipc_close(base). dl_can_access_peer: hipDeviceCanAccessPeer.
+ * dl_ipc_close(base). dl_can_access_peer: hipDeviceCanAccessPeer; dl_enable_peer_access:
+ * hipDeviceEnablePeerAccess.
  * dl_xgmi_reduce_sgd: on rank `rank` of n (<= 8), for packed elements [lo, lo+len) (this rank's
  * shard; lo, len multiples of 4, buffers 16-B aligned): g = (Σ_q wires[q][k] in rank order)/n,
  * Nesterov SGD on thetas[rank][k] and mom[k - lo], then thetas[q][k] = θ for every q. wires /
@@ -230,6 +231,8 @@ DL_API int dl_ipc_handle(const void* ptr, void* handle, int64_t* offset);
 DL_API int dl_ipc_open(const void* handle, void** base);
 DL_API int dl_ipc_close(void* base);
 DL_API int dl_can_access_peer(int32_t device, int32_t peer, int32_t* can);
+/* hipDeviceEnablePeerAccess(peer) from the current device; already enabled is success */
+DL_API int dl_enable_peer_access(int32_t peer);
 DL_API int dl_xgmi_reduce_sgd(const uint64_t* wires, const uint64_t* thetas, int32_t n,
                               int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
                               float momentum, int32_t nesterov, int32_t first_step,
