@@ -109,3 +109,15 @@ def test_load_state_dict_rejects_other_trees():
     st["theta"] = st["theta"][:-1]
     with pytest.raises(ValueError, match="does not match"):
         e.load_state_dict(st)
+
+
+def test_direct_exchange_arguments():
+    _, params = _micro_params()
+    with pytest.raises(ValueError, match="exchange"):
+        OuterSync(params, world_size=1, exchange="tcp")
+    with pytest.raises(ValueError, match="fp32 wire"):
+        OuterSync(params, world_size=1, exchange="xgmi", wire_dtype=torch.bfloat16)
+    e = OuterSync(params, world_size=1, exchange="xgmi")  # one rank: no peers to map
+    assert e.xgmi and not e.sharded and e.peers.ok
+    with pytest.raises(RuntimeError, match="exchange='xgmi'"):
+        e.apply()
