@@ -4,25 +4,24 @@ One `OuterSync` per DP replica (one process per GPU). It performs, for the whole
 `src/train.py:261-269` does per tensor on the CPU:
 
     compute_pseudo_gradient   (src/utils.py:218-221)  -> dl_delta_pack   wire = θ_outer - inner
-    sync_gradients            (src/comm.py:117-123)   -> RCCL all_reduce(SUM) of each bucket
-    outer_optimizer.step()    (src/train.py:267)      -> dl_unpack_sgd   g = wire/n; Nesterov SGD
-    sync_inner_model          (src/utils.py:223-226)  -> (fused in dl_unpack_sgd) inner = θ
+    sync_gradients            (src/comm.py:117-123)   -> the exchange below (Σ over replicas, /n)
+    outer_optimizer.step()    (src/train.py:267)      -> Nesterov SGD (torch's arithmetic)
+    sync_inner_model          (src/utils.py:223-226)  -> inner = θ
 
-With n > 1 replicas and an fp32 wire the default is the sharded variant of SURVEY §8e
-(shard=True): per bucket
-reduce-scatter of the wire -> dl_shard_sgd on this peer's 1/n (θ and momentum shards, ZeRO-1
-style) -> all-gather of θ -> dl_scatter into the inner params. Same bus bytes as the
-all-reduce; HBM traffic per peer 20 + 20/n B/param instead of 36, momentum memory 4P/n.
+Exchange variants, all bucketed and pipelined across buckets:
+  one replica        dl_delta_sgd: delta, SGD and copy-back in one pass (24 B/param);
+                     fuse_single=False keeps BASELINE config #2's dl_delta_pack -> dl_unpack_sgd
+  sharded            (default for n > 1 with the fp32 wire) RCCL reduce-scatter ->
+                     dl_shard_sgd on this peer's 1/n (θ and momentum shards) -> RCCL all-gather
+                     of θ -> dl_scatter; HBM 20 + 20/n B/param, momentum 4P/n
+  replicated         (shard=False; the bf16 wire's default) RCCL all-reduce -> dl_unpack_sgd
+                     (/n + SGD + copy-back, 24 B/param) on every replica
+  int8 wire          dl_delta_q8 -> all_to_all -> dl_q8_reduce -> all_gather -> dl_unpack_sgd_q8
+  direct (xgmi)      exchange="xgmi": IPC-mapped peers, one dl_xgmi_reduce_sgd per rank
 
-With one replica (no all-reduce, src/comm.py:118-119) the default is a single pass,
-dl_delta_sgd: the delta stays in registers (24 instead of 36 B/param); fuse_single=False
-keeps the two-kernel pipeline (BASELINE config #2's delta+pack -> unpack).
-
-Layout in HBM (DESIGN.md "Data layout"): θ_outer, momentum and the wire buffer are packed
-fp32 (wire optionally bf16) arrays in parameters() order with 256-B-aligned segments; the
-inner parameters stay where PyTorch allocated them and are reached through a device pointer
-table. With n > 1 replicas the buckets are pipelined: pack(b+1) and unpack(b-1) run on the
-compute stream while RCCL reduces bucket b on its own stream.
+Layout in HBM: θ_outer, momentum and the wire are packed arrays in
+parameters() order with 256-B-aligned segments; the inner parameters stay where PyTorch
+allocated them and are reached through a device pointer table.
 """
 from __future__ import annotations
 
@@ -238,8 +237,11 @@ class OuterSync:
         return self._shard(self.th_shard, bucket)
 
     def _local(self) -> bool:
-        # one replica and no process group: both collectives are identities (plain copies)
-        return self.world_size == 1 and not dist.is_initialized()
+        # one replica: both collectives are identities (plain copies) -- unless a one-rank
+        # process group is there to carry them (the single-rank RCCL transport test)
+        if self.world_size != 1:
+            return False
+        return not dist.is_initialized() or dist.get_world_size(self.group) != 1
 
     def reduce_scatter(self, bucket: int, async_op: bool = True):
         """SUM reduce-scatter of one wire bucket: this peer receives the sum of its 1/n."""
