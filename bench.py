@@ -263,6 +263,58 @@ def parity_check(dev, ws, rank, wire):
             "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
 
 
+def xgmi_link_probe(dev, ws, rank, reps=5, mib=256):
+    """Peer read rates through IPC-mapped buffers (what the 153 GB/s per link
+    means): every rank at once reads `mib` MiB from its ring neighbour (one direction of one
+    link each), then `mib` MiB from every peer at once (all links incoming), then the same
+    amount from its own HBM; max time over ranks."""
+    import ctypes
+
+    import numpy as np
+
+    from diloco_amd.xgmi import PeerMap
+
+    n = (mib << 20) // 4
+    buf = torch.empty(n, device=dev)
+    synth.fill_device(buf, 3, rank, 0.0, 1.0)
+    dst = torch.empty(max(1, ws - 1) * n, device=dev)
+    pm = PeerMap({"buf": buf}, None, dev)
+    if not pm.ok:
+        return {"ok": False, "error": pm.reason}
+    tab = pm.table("buf")
+    p64 = ctypes.POINTER(ctypes.c_uint64)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def timed(srcs):
+        arr = np.asarray(srcs, dtype=np.uint64)
+        _sync(ws)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            _lib.call("dl_peer_gather", arr.ctypes.data_as(p64), len(srcs), n * 4,
+                      dst.data_ptr(), stream)
+        e1.record()
+        e1.synchronize()
+        ms = _max_over_ranks(e0.elapsed_time(e1) / reps, dev, ws)
+        return round(len(srcs) * n * 4 / (ms * 1e-3) / 1e9, 1)
+
+    one = timed([int(tab[(rank + 1) % ws])])
+    want = torch.empty(n, device=dev)  # the neighbour's buffer, regenerated here
+    synth.fill_device(want, 3, (rank + 1) % ws, 0.0, 1.0)
+    ok = bool(torch.equal(dst[:n], want))  # the peer's bytes arrived intact
+    del want
+    peers = [int(tab[q]) for q in range(ws) if q != rank]
+    allp = timed(peers)
+    local = timed([int(tab[rank])])
+    _sync(ws)
+    pm.close()
+    _sync(ws)
+    return {"bytes_per_source": n * 4, "one_peer_read_GBs": one,
+            "all_peers_read_GBs": allp, "local_hbm_read_GBs": local, "peers": ws - 1,
+            "note": "read rate per rank (GB/s of source bytes), all ranks concurrently; "
+                    "one_peer = ring neighbour = one direction of one link", "ok": ok}
+
+
 def parity_xgmi(dev, ws, rank):
     """The direct exchange (exchange='xgmi') against the RCCL sharded step on the tiny tree,
     2 outer steps: θ and momentum normwise <= 1e-6 per tensor (bit-exact at n <= 2; the direct
@@ -696,6 +748,7 @@ def main():
             extra[f"{spec.name}_xgmi_exchange"] = _brief(r) if "value" in r else r
             if parity is not None:
                 parity["xgmi"] = _guard(parity_xgmi, dev, ws, rank)
+            extra["xgmi_link_probe"] = _guard(xgmi_link_probe, dev, ws, rank)
     if rank == 0:
         line = {
             "metric": METRIC,

@@ -466,6 +466,25 @@ DL_API int dl_enable_peer_access(int32_t peer) {
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_enable_peer_access");
 }
 
+DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each, void* dst,
+                          dl_stream_t s) {
+  if (!srcs || !dst) return fail(DL_E_ARG, "dl_peer_gather: null argument");
+  if (nsrc < 1 || nsrc > dl::kMaxPeers)
+    return fail(DL_E_ARG, "dl_peer_gather: %d sources (1..%d)", nsrc, dl::kMaxPeers);
+  if (bytes_each < 0 || bytes_each % 16 || bytes_each / 16 > INT32_MAX)
+    return fail(DL_E_ARG, "dl_peer_gather: bytes_each %lld (multiple of 16, < 32 GiB)",
+                (long long)bytes_each);
+  DL_TRY(check_packed(dst, "dl_peer_gather", "dst"));
+  dl::XgmiPeers p{};
+  for (int32_t i = 0; i < nsrc; ++i) {
+    p.wire[i] = reinterpret_cast<const float*>(srcs[i]);
+    DL_TRY(check_packed(p.wire[i], "dl_peer_gather", "source"));
+  }
+  hipError_t e = dl::launch_peer_gather(p, nsrc, int32_t(bytes_each / 16),
+                                        static_cast<float*>(dst), static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_peer_gather");
+}
+
 DL_API int dl_xgmi_reduce_sgd(const uint64_t* wires, const uint64_t* thetas, int32_t n,
                               int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
                               float momentum, int32_t nesterov, int32_t first_step,

@@ -81,7 +81,28 @@ hipError_t launch_n(const XgmiPeers& p, int32_t rank, int64_t lo, int64_t len, f
   return hipGetLastError();
 }
 
+// link probe: dst[i*each + k] = srcs[i][k] for every source, workgroups interleaved across the
+// sources so all of them stream at once (each4 = float4 per source, < 2^31)
+__global__ void __launch_bounds__(kThreads)
+    k_peer_gather(XgmiPeers p, int32_t nsrc, int32_t each4, float* __restrict__ dst) {
+  const int32_t i = int32_t(blockIdx.x) % nsrc;
+  const int32_t per = int32_t(gridDim.x) / nsrc;
+  const float* src = p.wire[i];
+  float* out = dst + int64_t(i) * each4 * 4;
+  for (int32_t v = (int32_t(blockIdx.x) / nsrc) * kThreads + int32_t(threadIdx.x); v < each4;
+       v += per * kThreads)
+    stf4<true>(out, v, ldf4<true>(src, v));
+}
+
 }  // namespace
+
+hipError_t launch_peer_gather(const XgmiPeers& p, int32_t nsrc, int32_t each4, float* dst,
+                              hipStream_t s) {
+  if (nsrc <= 0 || each4 <= 0) return hipSuccess;
+  const int32_t per = 2048;  // workgroups per source
+  hipLaunchKernelGGL(k_peer_gather, dim3(per * nsrc), dim3(kThreads), 0, s, p, nsrc, each4, dst);
+  return hipGetLastError();
+}
 
 hipError_t launch_xgmi_reduce_sgd(const XgmiPeers& p, int32_t n, int32_t rank, int64_t lo,
                                   int64_t len, float* mom, SgdArgs a, hipStream_t s) {

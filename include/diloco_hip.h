@@ -233,6 +233,10 @@ DL_API int dl_ipc_close(void* base);
 DL_API int dl_can_access_peer(int32_t device, int32_t peer, int32_t* can);
 /* hipDeviceEnablePeerAccess(peer) from the current device; already enabled is success */
 DL_API int dl_enable_peer_access(int32_t peer);
+/* link probe: dst[i*bytes_each ...] <- srcs[i][0 .. bytes_each) for i < nsrc (<= 8), all
+ * sources streamed at once by one kernel (measures per-link and aggregate peer read rates) */
+DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each, void* dst,
+                          dl_stream_t stream);
 DL_API int dl_xgmi_reduce_sgd(const uint64_t* wires, const uint64_t* thetas, int32_t n,
                               int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
                               float momentum, int32_t nesterov, int32_t first_step,

@@ -667,3 +667,19 @@ def test_tensor_larger_than_int32_elements():
         got = params[1][lo:lo + n].cpu().numpy()
         assert got.size == n and got.tobytes() == st.theta[0].tobytes(), lo
     ea.close()
+
+
+def test_peer_gather_copies_every_source():
+    """dl_peer_gather (the xGMI link probe's kernel) with local sources: dst holds each source's
+    bytes in order, ragged lengths included."""
+    import ctypes
+
+    for nsrc, each in ((1, 16), (3, 4096 * 4 + 48), (8, 1 << 20)):
+        srcs = [torch.arange(each // 4, dtype=torch.float32, device=DEV) + 1000 * i
+                for i in range(nsrc)]
+        dst = torch.full((nsrc * each // 4,), -1.0, device=DEV)
+        arr = np.asarray([t.data_ptr() for t in srcs], dtype=np.uint64)
+        _lib.call("dl_peer_gather", arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), nsrc,
+                  each, dst.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(dst, torch.cat(srcs)), (nsrc, each)
