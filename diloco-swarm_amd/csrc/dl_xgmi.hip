@@ -85,13 +85,25 @@ hipError_t launch_n(const XgmiPeers& p, int32_t rank, int64_t lo, int64_t len, f
 // sources so all of them stream at once (each4 = float4 per source, < 2^31)
 __global__ void __launch_bounds__(kThreads)
     k_peer_gather(XgmiPeers p, int32_t nsrc, int32_t each4, float* __restrict__ dst) {
+  constexpr int U = 4;  // float4 loads in flight per lane
   const int32_t i = int32_t(blockIdx.x) % nsrc;
   const int32_t per = int32_t(gridDim.x) / nsrc;
   const float* src = p.wire[i];
   float* out = dst + int64_t(i) * each4 * 4;
-  for (int32_t v = (int32_t(blockIdx.x) / nsrc) * kThreads + int32_t(threadIdx.x); v < each4;
-       v += per * kThreads)
-    stf4<true>(out, v, ldf4<true>(src, v));
+  for (int32_t v0 = (int32_t(blockIdx.x) / nsrc) * kThreads * U; v0 < each4;
+       v0 += per * kThreads * U) {
+    float4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t v = v0 + u * kThreads + int32_t(threadIdx.x);
+      if (v < each4) x[u] = ldf4<true>(src, v);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t v = v0 + u * kThreads + int32_t(threadIdx.x);
+      if (v < each4) stf4<true>(out, v, x[u]);
+    }
+  }
 }
 
 }  // namespace
@@ -99,7 +111,7 @@ __global__ void __launch_bounds__(kThreads)
 hipError_t launch_peer_gather(const XgmiPeers& p, int32_t nsrc, int32_t each4, float* dst,
                               hipStream_t s) {
   if (nsrc <= 0 || each4 <= 0) return hipSuccess;
-  const int32_t per = 2048;  // workgroups per source
+  const int32_t per = 1024;  // workgroups per source
   hipLaunchKernelGGL(k_peer_gather, dim3(per * nsrc), dim3(kThreads), 0, s, p, nsrc, each4, dst);
   return hipGetLastError();
 }
