@@ -471,7 +471,7 @@ DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each
   if (!srcs || !dst) return fail(DL_E_ARG, "dl_peer_gather: null argument");
   if (nsrc < 1 || nsrc > dl::kMaxPeers)
     return fail(DL_E_ARG, "dl_peer_gather: %d sources (1..%d)", nsrc, dl::kMaxPeers);
-  if (bytes_each < 0 || bytes_each % 16 || bytes_each / 16 > INT32_MAX)
+  if (bytes_each < 0 || bytes_each % 16 || bytes_each / 16 > INT32_MAX - (1 << 24))
     return fail(DL_E_ARG, "dl_peer_gather: bytes_each %lld (multiple of 16, < 32 GiB)",
                 (long long)bytes_each);
   DL_TRY(check_packed(dst, "dl_peer_gather", "dst"));
