@@ -35,8 +35,8 @@ def main():
     # sharded step's dl_shard_sgd (one replica: the shard is the whole bucket)
     q8 = OuterSync(params, world_size=1, wire_dtype=torch.int8, bucket_cap_elems=0)
     sh = OuterSync(params, world_size=1, shard=True, bucket_cap_elems=0)
-    for e in (q8, sh):
-        assert e.tree.n_buckets == 1
+    xg = OuterSync(params, world_size=1, exchange="xgmi")  # n = 1: the fused kernel, local
+    for e in (q8, sh, xg):
         for _ in range(reps + 1):
             e.step()
     torch.cuda.synchronize()
