@@ -24,7 +24,6 @@ def short(name):
     for k, v in names.items():
         if k in name:
             first = ((k in ("UnpackSgd", "k_flat") and ", 1>" in name)
-                     or (k == "k_xgmi_reduce_sgd" and False)
                      or (k == "DeltaSgd" and "DeltaSgd<1>" in name)
                      or (k == "UnpackSgdQ8" and "UnpackSgdQ8<1>" in name))
             return v + ("_first" if first else "")
