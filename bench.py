@@ -76,12 +76,13 @@ def setup_dist(n_gpus):
     return ws, rank, dev
 
 
-def build(spec, dev, rank, wire, cap, fuse=False, shard=None, exchange="rccl"):
+def build(spec, dev, rank, wire, cap, fuse=False, shard=None, exchange="rccl", tile=None):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree_device(spec, dev)
     params = [t.view(s) for t, s in zip(theta0, shapes)]
     eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=wire,
-                    bucket_cap_elems=cap, fuse_single=fuse, shard=shard, exchange=exchange)
+                    bucket_cap_elems=cap, fuse_single=fuse, shard=shard, exchange=exchange,
+                    **({} if tile is None else {"tile_chunks": tile}))
     # inner = θ_0 + this rank's noise (stands in for H inner steps)
     synth.inner_tree_device([p.view(-1) for p in params], 1, rank, out=[p.view(-1) for p in params])
     return eng
@@ -110,11 +111,11 @@ def kernel_entry(bytes_per_launch, ms, traffic=None, bound="hbm", peak=HBM_PEAK_
 
 
 def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loops=True,
-             shard=None, exchange="rccl"):
+             shard=None, exchange="rccl", tile=None):
     """Timed region (K outer steps, nothing else on the stream), then an instrumented pass of
     K more steps with HIP events between the kernels on the stream they run on (events in the
     timed region would cost the step ~35 us each), then the same kernels back to back."""
-    eng = build(spec, dev, rank, wire, cap, fuse, shard, exchange)
+    eng = build(spec, dev, rank, wire, cap, fuse, shard, exchange, tile)
     P = spec.total()
     for _ in range(max(warmup, 1)):  # >= 1: the timed steps run the steady-state SGD mode
         eng.step()
@@ -150,7 +151,12 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
            "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
            "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * P / (dt / steps) / 1e9,
            "wire": "bf16" if wire == torch.bfloat16 else "f32",
-           "variant": ("direct peer-access exchange (IPC, dl_xgmi_reduce_sgd)" if eng.xgmi
+           "tile_chunks": eng.tile_chunks if single and not fuse else None,
+           "variant": ("one replica: dl_delta_sgd (one pass)" if single and fuse
+                       else ("one replica: dl_delta_pack -> dl_unpack_sgd"
+                             + (f", tiles of {eng.tile_chunks} chunks" if eng.tile_chunks
+                                else ", whole-range launches")) if single
+                       else "direct peer-access exchange (IPC, dl_xgmi_reduce_sgd)" if eng.xgmi
                        else "reduce_scatter -> shard SGD -> all_gather" if eng.sharded
                        else "all_reduce -> replicated SGD")}
     if single and fuse:
@@ -667,8 +673,51 @@ def _guard(fn, *a, **k):
 
 def _brief(r):
     keep = ("value", "ms_per_step", "roofline", "kernels", "buckets", "params", "wire", "variant",
-            "wire_bytes_per_param", "bus_bytes_per_step")
+            "wire_bytes_per_param", "bus_bytes_per_step", "tile_chunks")
     return {k: r[k] for k in keep if k in r}
+
+
+class _Emitter:
+    """The one JSON line, assembled as the legs finish, printed exactly once by rank 0.
+
+    A watchdog (every rank, same deadline) bounds the whole run: if a side leg hangs (an RCCL
+    collective or a peer-access kernel at N > 1 that no test box can rehearse), the line with
+    the headline and every leg finished so far is printed, naming the leg that was running,
+    and every rank leaves with os._exit -- the driver still gets its measurement instead of a
+    killed run. Legs that would start after the soft budget are skipped and listed."""
+
+    def __init__(self, rank, deadline_s):
+        import threading
+
+        self.rank, self.t0, self.deadline = rank, time.perf_counter(), deadline_s
+        self.line, self.running, self.skipped = None, "headline", []
+        self.lock = threading.Lock()
+        self.done = False
+        self.timer = threading.Timer(deadline_s, self._fire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def elapsed(self):
+        return time.perf_counter() - self.t0
+
+    def emit(self):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.rank == 0 and self.line is not None:
+                if self.skipped:
+                    self.line["skipped_legs"] = self.skipped
+                print(json.dumps(self.line), flush=True)
+
+    def _fire(self):
+        log(f"watchdog: {self.deadline:.0f} s reached while running {self.running!r}")
+        if self.line is not None:
+            self.line["incomplete"] = {"leg": self.running, "deadline_s": self.deadline}
+        self.emit()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if self.line is not None else 3)
 
 
 def main():
@@ -691,100 +740,127 @@ def main():
                     help="headline tree only (for rocprofv3 runs of the same kernels)")
     ap.add_argument("--no-b2b", action="store_true",
                     help="skip the back-to-back kernel loops (rocprofv3 averages = in-step launches)")
+    ap.add_argument("--deadline", type=float,
+                    default=float(os.environ.get("DILOCO_BENCH_DEADLINE_S", "420")),
+                    help="hard wall-clock bound of the whole run (s); side legs stop starting "
+                         "at 70 %% of it")
     a = ap.parse_args()
 
+    em = _Emitter(int(os.environ.get("RANK", "0")), a.deadline)
+    soft = 0.7 * a.deadline
     ws, rank, dev = setup_dist(a.gpus)
     wire = torch.bfloat16 if a.wire == "bf16" else torch.float32
     cap = (a.bucket_mb << 20) // 4
     _lib.load()
     spec = get_tree(a.tree)
     log(f"rank {rank}/{ws} tree {spec.name} ({spec.total()} params) wire {a.wire}")
+    # headline at N = 1: whole-range launches (tile 0), so the per-kernel figures and the
+    # rocprofv3 averages describe the same launches; cache blocking is neutral on T125
+    # (tools/tile_ab.py) and is what the T1.3B leg below runs (OuterSync's default tile)
     main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap,
-                        b2b_loops=not a.no_b2b)
-    extra, parity, dropin, cpu = {}, None, None, None
+                        b2b_loops=not a.no_b2b, tile=0)
+    extra, parity = {}, {}
+    em.line = {
+        "metric": METRIC,
+        "value": round(main_res["value"], 3),
+        "unit": "GB/s",
+        "n_gpus": ws,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(main_res["ms_per_step"], 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if a.wire == "f32" else "f32 (bf16 wire)",
+        "data": "synthetic (counter-based GPT-2-shaped tree, SURVEY.md §8d)",
+        "config": {
+            "workload": (f"DiLoCo outer step, {spec.name} tree per rank: delta_pack -> "
+                         + ("RCCL reduce_scatter -> shard_sgd (1/n of θ, momentum) -> RCCL "
+                            "all_gather(θ) -> scatter to inner (bucketed, pipelined)"
+                            if ws > 1 else "unpack_sgd (+copy to inner)")),
+            "tree": spec.name, "params": main_res["params"], "tensors": main_res["tensors"],
+            "wire": a.wire, "buckets": main_res["buckets"], "chunks": main_res["chunks"],
+            "parallelism": f"dp{ws}",
+        },
+        "roofline": main_res["roofline"],
+        "cpu_baseline": None,
+        "kernels": main_res.get("kernels"),
+        "kernels_b2b": main_res.get("kernels_b2b"),
+        "parity": None if a.no_parity or a.only_headline else parity,
+        "dropin_pcie": None,
+        "extra": extra,
+        "host": platform.node(),
+    }
+    log(f"headline done at {em.elapsed():.1f} s")
+
+    def leg(name, fn, *args, into=extra, brief=True):
+        """One side leg, in the same order on every rank; skipped (on every rank alike: the
+        decision uses the max over ranks of the elapsed time) past the soft budget."""
+        t = _max_over_ranks(em.elapsed(), dev, ws)
+        if t > soft:
+            em.skipped.append(name)
+            log(f"skipping {name}: {t:.0f} s elapsed > soft budget {soft:.0f} s")
+            return None
+        em.running = name
+        r = _guard(fn, *args)
+        if brief and isinstance(r, dict) and "value" in r:
+            r = _brief(r)
+        into[name] = r
+        log(f"{name} done at {em.elapsed():.1f} s")
+        return r
+
     if not a.only_headline:
         if ws == 1:
-            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, cap, True)
-            extra[f"{spec.name}_fused_single"] = _brief(r) if "value" in r else r
+            leg(f"{spec.name}_fused_single", run_tree, spec, dev, ws, rank, a.steps, a.warmup,
+                wire, cap, True)
         if a.extra_tree != "none" and a.extra_tree != a.tree:
             es = get_tree(a.extra_tree)
             ks = max(3, a.steps // 4)
-            r = _guard(run_tree, es, dev, ws, rank, ks, 1, wire, cap)
-            extra[es.name] = _brief(r) if "value" in r else r
+            leg(es.name, run_tree, es, dev, ws, rank, ks, 1, wire, cap)
             if wire == torch.float32:  # BASELINE config #5: bf16 wire + SGD fused into unpack
-                r = _guard(run_tree, es, dev, ws, rank, ks, 1, torch.bfloat16, cap)
-                extra[f"{es.name}_bf16_wire"] = _brief(r) if "value" in r else r
-                r = _guard(run_q8, es, dev, ws, rank, ks, 1, cap)  # §8f row 4: int8 wire
-                extra[f"{es.name}_int8_wire"] = _brief(r) if "value" in r else r
+                leg(f"{es.name}_bf16_wire", run_tree, es, dev, ws, rank, ks, 1, torch.bfloat16,
+                    cap)
+                leg(f"{es.name}_int8_wire", run_q8, es, dev, ws, rank, ks, 1, cap)  # §8f row 4
         if ws > 1:
             # the replicated variant (all-reduce -> SGD on every peer) beside the sharded headline
-            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, cap, False,
-                       False, False)
-            extra[f"{spec.name}_allreduce_variant"] = _brief(r) if "value" in r else r
+            leg(f"{spec.name}_allreduce_variant", run_tree, spec, dev, ws, rank, a.steps,
+                a.warmup, wire, cap, False, False, False)
             # bucket size for the xGMI pipeline: 64 MiB buckets (more overlap, more calls)
-            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, 16 << 20, False,
-                       False)
-            extra[f"{spec.name}_bucket64MiB"] = _brief(r) if "value" in r else r
-            extra[f"{spec.name}_dp_grad_sync"] = _guard(gradsync_rate, spec, dev, ws, rank,
-                                                        max(3, a.steps // 2))
+            leg(f"{spec.name}_bucket64MiB", run_tree, spec, dev, ws, rank, a.steps, a.warmup,
+                wire, 16 << 20, False, False)
+            leg(f"{spec.name}_dp_grad_sync", gradsync_rate, spec, dev, ws, rank,
+                max(3, a.steps // 2), brief=False)
         if not a.no_parity:
-            parity = {"f32": _guard(parity_check, dev, ws, rank, torch.float32),
-                      "bf16": _guard(parity_check, dev, ws, rank, torch.bfloat16),
-                      "int8": _guard(parity_q8, dev, ws, rank),
-                      "sharded": _guard(parity_sharded, dev, ws, rank)}
+            leg("f32", parity_check, dev, ws, rank, torch.float32, into=parity, brief=False)
+            leg("bf16", parity_check, dev, ws, rank, torch.bfloat16, into=parity, brief=False)
+            leg("int8", parity_q8, dev, ws, rank, into=parity, brief=False)
+            leg("sharded", parity_sharded, dev, ws, rank, into=parity, brief=False)
         if a.p2p:
-            extra["p2p_device_transport"] = _guard(p2p_rate, spec, dev, ws, rank, 10)
+            leg("p2p_device_transport", p2p_rate, spec, dev, ws, rank, 10, brief=False)
         if not a.no_dropin:
-            dropin = _guard(dropin_rate, spec, dev, ws, rank, 5)
-            extra[f"{spec.name}_dropin_device"] = _guard(dropin_rate, spec, dev, ws, rank, 10,
-                                                         "device")
-        if rank == 0 and ws == 1 and not a.no_cpu_baseline:
+            em.line["dropin_pcie"] = leg("dropin_pcie", dropin_rate, spec, dev, ws, rank, 5,
+                                         into={}, brief=False)
+            leg(f"{spec.name}_dropin_device", dropin_rate, spec, dev, ws, rank, 10, "device",
+                brief=False)
+        if ws == 1 and not a.no_cpu_baseline:
+            # rank 0 at N = 1 only (the reference's CPU path on this host's cores)
+            em.running = "cpu_baseline"
             log("timing the CPU baseline")
-            cpu = cpu_baseline(spec)
+            em.line["cpu_baseline"] = cpu_baseline(spec)
         if ws > 1 and not a.no_xgmi:
             # last: the direct peer-access exchange (IPC-mapped wires / θ, one fused kernel)
-            r = _guard(run_tree, spec, dev, ws, rank, a.steps, a.warmup, torch.float32, cap,
-                       False, False, None, "xgmi")
-            extra[f"{spec.name}_xgmi_exchange"] = _brief(r) if "value" in r else r
-            if parity is not None:
-                parity["xgmi"] = _guard(parity_xgmi, dev, ws, rank)
-            extra["xgmi_link_probe"] = _guard(xgmi_link_probe, dev, ws, rank)
-    if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(main_res["value"], 3),
-            "unit": "GB/s",
-            "n_gpus": ws,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(main_res["ms_per_step"], 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32" if a.wire == "f32" else "f32 (bf16 wire)",
-            "data": "synthetic (counter-based GPT-2-shaped tree, SURVEY.md §8d)",
-            "config": {
-                "workload": (f"DiLoCo outer step, {spec.name} tree per rank: delta_pack -> "
-                             + ("RCCL reduce_scatter -> shard_sgd (1/n of θ, momentum) -> RCCL "
-                                "all_gather(θ) -> scatter to inner (bucketed, pipelined)"
-                                if ws > 1 else "unpack_sgd (+copy to inner)")),
-                "tree": spec.name, "params": main_res["params"], "tensors": main_res["tensors"],
-                "wire": a.wire, "buckets": main_res["buckets"], "chunks": main_res["chunks"],
-                "parallelism": f"dp{ws}",
-            },
-            "roofline": main_res["roofline"],
-            "cpu_baseline": cpu,
-            "kernels": main_res.get("kernels"),
-            "kernels_b2b": main_res.get("kernels_b2b"),
-            "parity": parity,
-            "dropin_pcie": dropin,
-            "extra": extra or None,
-            "host": platform.node(),
-        }
-        print(json.dumps(line), flush=True)
+            leg(f"{spec.name}_xgmi_exchange", run_tree, spec, dev, ws, rank, a.steps,
+                a.warmup, torch.float32, cap, False, False, None, "xgmi")
+            if not a.no_parity:
+                leg("xgmi", parity_xgmi, dev, ws, rank, into=parity, brief=False)
+            leg("xgmi_link_probe", xgmi_link_probe, dev, ws, rank, brief=False)
+    em.running = "teardown"
+    em.line["wall_s"] = round(em.elapsed(), 1)
+    em.emit()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+    em.timer.cancel()
 
 
 if __name__ == "__main__":

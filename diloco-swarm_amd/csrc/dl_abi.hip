@@ -397,6 +397,41 @@ DL_API int dl_delta_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_sgd");
 }
 
+// a2 -> (one peer: the exchange is the identity, src/comm.py:118-119) -> a3-a5, cache-blocked:
+// the tree is walked in tiles of tile_chunks chunks and each tile runs dl_delta_pack then
+// dl_unpack_sgd, so the wire and θ bytes the pack just touched are re-read by the unpack from
+// the 256 MiB Infinity Cache instead of HBM. Elementwise work: bit-identical to the two
+// whole-range launches for every tile size.
+DL_API int dl_pack_sgd_tiled(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer, void* wire,
+                             int32_t wire_dtype, float* mom, float lr, float momentum,
+                             int32_t nesterov, int32_t first_step, int32_t tile_chunks,
+                             dl_stream_t s) {
+  dl::Launch P, U;
+  DL_TRY(make_launch(t, b, s, &P, "dl_pack_sgd_tiled", kAutoDelta));
+  DL_TRY(make_launch(t, b, s, &U, "dl_pack_sgd_tiled", kAutoUnpackSgd));
+  DL_TRY(check_slot(t, inner_slot, "dl_pack_sgd_tiled"));
+  DL_TRY(check_packed(outer, "dl_pack_sgd_tiled", "outer"));
+  DL_TRY(check_packed(wire, "dl_pack_sgd_tiled", "wire"));
+  DL_TRY(check_dtype(wire_dtype, "dl_pack_sgd_tiled"));
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_pack_sgd_tiled", "momentum"));
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_pack_sgd_tiled: Nesterov momentum requires a momentum");
+  if (tile_chunks < 0) return fail(DL_E_ARG, "dl_pack_sgd_tiled: tile_chunks %d", tile_chunks);
+  const dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  const int32_t c0 = P.c0, c1 = P.c1;
+  const int32_t step = tile_chunks > 0 ? tile_chunks : (c1 - c0 > 0 ? c1 - c0 : 1);
+  for (int32_t c = c0; c < c1; c += step) {
+    const int32_t e = c1 - c < step ? c1 : c + step;
+    P.c0 = U.c0 = c;
+    P.c1 = U.c1 = e;
+    hipError_t err = dl::launch_delta_pack(P, inner_slot, outer, wire, wire_dtype);
+    if (err == hipSuccess)
+      err = dl::launch_unpack_sgd(U, wire, wire_dtype, 1, outer, mom, a, inner_slot);
+    if (err != hipSuccess) return hip_fail(err, "dl_pack_sgd_tiled");
+  }
+  return DL_OK;
+}
+
 DL_API int dl_shard_sgd(const void* wire, int32_t wire_dtype, int32_t divisor, float* outer,
                         float* mom, int64_t n, float lr, float momentum, int32_t nesterov,
                         int32_t first_step, dl_stream_t s) {

@@ -72,6 +72,14 @@ class HipKernels:
         _lib.call("dl_delta_sgd", tree.handle, bucket, inner_slot, theta.data_ptr(), _ptr(mom),
                   float(lr), float(momentum), int(nesterov), int(first), _s(theta))
 
+    def pack_sgd_tiled(self, tree, bucket, inner_slot, theta, wire, mom, lr, momentum,
+                       nesterov, first, tile_chunks) -> None:
+        """One peer: delta_pack then unpack_sgd (divisor 1) tile by tile (Infinity-Cache
+        blocking); the same results as the two whole-range launches."""
+        _lib.call("dl_pack_sgd_tiled", tree.handle, bucket, inner_slot, theta.data_ptr(),
+                  wire.data_ptr(), wire_code(wire.dtype), _ptr(mom), float(lr), float(momentum),
+                  int(nesterov), int(first), int(tile_chunks), _s(theta))
+
     def shard_sgd(self, wire, divisor, theta, mom, lr, momentum, nesterov, first) -> None:
         """Flat 1/n shard after a reduce-scatter (wire, theta, mom: equal-length views)."""
         _lib.call("dl_shard_sgd", wire.data_ptr(), wire_code(wire.dtype), int(divisor),

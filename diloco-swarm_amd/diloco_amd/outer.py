@@ -35,6 +35,12 @@ from .kernels import Q8_SLOT, default_kernels
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER
 
 ALL = _lib.ALL_BUCKETS
+# Tile of dl_pack_sgd_tiled: 4096 chunks = 16 Mi elements, 64 MiB per stream. Measured
+# (tools/tile_ab.py, profiles/r01_tile_ab_*.json): T1.3B one-replica step 8.25 -> 7.55 ms
+# (the step re-reads wire and θ of the tile from the Infinity Cache); T125 unchanged (0.694
+# vs 0.697 ms: its whole-range step already reuses the cache across the step boundary).
+# Smaller tiles lose: every extra launch boundary costs ≈ 2 µs (256-chunk tiles: 1.18 ms).
+DEFAULT_TILE_CHUNKS = 4096
 
 
 def pipelined_buckets(n_buckets: int, pack: Callable[[int], None],
@@ -84,6 +90,7 @@ class OuterSync:
         shard: Optional[bool] = None,
         rank: Optional[int] = None,
         exchange: str = "rccl",
+        tile_chunks: int = DEFAULT_TILE_CHUNKS,
     ):
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
                                            for p in params]
@@ -97,6 +104,11 @@ class OuterSync:
         self.wire_dtype = wire_dtype
         # one replica: delta + SGD + copy-back in one pass (dl_delta_sgd), no wire round trip
         self.fuse_single = bool(fuse_single)
+        # one replica, two-kernel pipeline: pack/step tile by tile (dl_pack_sgd_tiled) so the
+        # step re-reads the wire and θ from the Infinity Cache; 0 = whole-range launches
+        if tile_chunks < 0:
+            raise ValueError(f"tile_chunks {tile_chunks} < 0")
+        self.tile_chunks = int(tile_chunks)
         self.group = group
         if world_size is None:
             world_size = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -359,6 +371,11 @@ class OuterSync:
             self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.delta_sgd(self.tree, ALL, SLOT_INNER, self.theta, self.mom, self.lr,
                              self.momentum, self.nesterov, self.steps_done == 0)
+        elif self.tile_chunks:
+            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+            self.k.pack_sgd_tiled(self.tree, ALL, SLOT_INNER, self.theta, self.wire, self.mom,
+                                  self.lr, self.momentum, self.nesterov, self.steps_done == 0,
+                                  self.tile_chunks)
         else:
             self.pseudo_gradient(ALL)
             self.apply(ALL)

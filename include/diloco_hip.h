@@ -143,6 +143,17 @@ DL_API int dl_delta_sgd(dl_tree_t tree, int32_t bucket, int32_t inner_slot, floa
                         float* mom_packed, float lr, float momentum, int32_t nesterov,
                         int32_t first_step, dl_stream_t stream);
 
+/* a2 -> a3 -> a4 -> a5 at ONE peer as the two-kernel pipeline (dl_delta_pack then
+ * dl_unpack_sgd with divisor 1; src/utils.py:221, src/comm.py:118-119, src/train.py:267,
+ * src/utils.py:226), cache-blocked: the bucket's chunk range is walked in tiles of
+ * tile_chunks chunks (0 = one tile), each tile packed then stepped, so the unpack re-reads
+ * the wire and θ bytes the pack just touched from the Infinity Cache. wire holds the
+ * pseudo-gradient afterwards. Bit-identical to the two whole-range launches. */
+DL_API int dl_pack_sgd_tiled(dl_tree_t tree, int32_t bucket, int32_t inner_slot,
+                             float* outer_packed, void* wire, int32_t wire_dtype,
+                             float* mom_packed, float lr, float momentum, int32_t nesterov,
+                             int32_t first_step, int32_t tile_chunks, dl_stream_t stream);
+
 /* Gather per-tensor fp32 (slot) into a packed buffer of dtype `dtype` (fp32 or bf16).
  * Used to pack device gradients (DP sync, src/comm.py:117-123 with device grads, called at
  * src/train.py:251) and to initialise the device θ_outer mirror (src/utils.py:215). */

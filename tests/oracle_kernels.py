@@ -87,6 +87,13 @@ class OracleKernels:
             if inner_slot >= 0:
                 _np(tree.slots[inner_slot][i])[:] = th
 
+    def pack_sgd_tiled(self, tree, bucket, inner_slot, theta, wire, mom, lr, momentum,
+                       nesterov, first, tile_chunks):
+        # tiling only changes the launch order of elementwise work: the two whole-range steps
+        self.delta_pack(tree, bucket, inner_slot, theta, wire)
+        self.unpack_sgd(tree, bucket, wire, 1, theta, mom, lr, momentum, nesterov, first,
+                        inner_slot)
+
     def delta_sgd(self, tree, bucket, inner_slot, theta, mom, lr, momentum, nesterov, first):
         for i in tree.segs(bucket):
             th = self._seg(tree, theta, i).copy()

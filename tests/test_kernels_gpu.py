@@ -297,6 +297,55 @@ def test_fused_single_peer_ragged_vs_two_kernel_path(momentum, nesterov):
         assert ea.theta.cpu().numpy().tobytes() == eb.theta.cpu().numpy().tobytes()
 
 
+@pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("momentum,nesterov", [(0.9, True), (0.9, False), (0.0, False)])
+def test_tiled_pack_sgd_equals_whole_range_launches(wire, momentum, nesterov):
+    """dl_pack_sgd_tiled (Infinity-Cache-blocked delta_pack -> unpack_sgd) is bit-identical to
+    the two whole-range launches for tiles of 1, 3 and 7 chunks (tiles cut tensors and end
+    inside ragged tails) and leaves the same wire."""
+    g0 = torch.Generator().manual_seed(11)
+    host = [torch.randn(n, generator=g0) for n in RAGGED]
+    ps = {t: [h.to(DEV) for h in host] for t in (0, 1, 3, 7)}
+    es = {t: OuterSync(p, momentum=momentum, nesterov=nesterov, world_size=1, wire_dtype=wire,
+                       fuse_single=False, tile_chunks=t) for t, p in ps.items()}
+    for _ in range(3):
+        noise = [torch.randn(n, generator=g0).to(DEV) * 1e-3 for n in RAGGED]
+        for t in es:
+            for p, z in zip(ps[t], noise):
+                p.add_(z)
+            es[t].step()
+        torch.cuda.synchronize()
+        ref = es[0]
+        for t in (1, 3, 7):
+            assert es[t].theta.cpu().numpy().tobytes() == ref.theta.cpu().numpy().tobytes(), t
+            assert es[t].wire.cpu().view(torch.int16 if wire == torch.bfloat16 else
+                                         torch.int32).numpy().tobytes() == \
+                ref.wire.cpu().view(torch.int16 if wire == torch.bfloat16 else
+                                    torch.int32).numpy().tobytes(), t
+            if momentum:
+                assert es[t].mom.cpu().numpy().tobytes() == ref.mom.cpu().numpy().tobytes()
+            for p, q in zip(ps[t], ps[0]):
+                assert p.cpu().numpy().tobytes() == q.cpu().numpy().tobytes(), t
+
+
+def test_tiled_pack_sgd_micro_matches_reference():
+    """The tiled one-replica pipeline reproduces the reference's micro-tree outer steps."""
+    spec = get_tree("micro")
+    theta0 = synth.outer_tree_device(spec, DEV)
+    shapes = [s for _, s in spec.params()]
+    params = [t.clone().view(s) for t, s in zip(theta0, shapes)]
+    e = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=2)
+    g = load_npz("micro_n1.npz")
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        e.step()
+        torch.cuda.synchronize()
+        assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert np.concatenate(_host(e.unpacked(e.mom))).tobytes() == g[f"buf_s{s}"].tobytes()
+        assert np.concatenate(_host(params)).tobytes() == g[f"theta_s{s}"].tobytes()
+
+
 def test_t13b_full_size_sampled_tensors_vs_oracle_and_fused():
     """BASELINE configs #4/#5 tree at full size (1.31 B params): the two-kernel path equals the
     one-pass kernel everywhere (size-independent property), and the largest (wte, 103 M),
