@@ -269,6 +269,35 @@ def parity_check(dev, ws, rank, wire):
             "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
 
 
+def rccl_reference(dev, ws, rank, elems, reps=5):
+    """What RCCL itself reaches on this node for the headline's bytes: one fp32 all_reduce
+    (SUM) of `elems` elements, and a reduce_scatter + all_gather pair of the same size,
+    back to back, max over ranks. busBW = 2(n-1)/n · bytes / t (the nccl-tests convention,
+    SURVEY §8d): the measured 'algorithmic all-reduce bandwidth' the exchange is held to."""
+    x = torch.ones(elems, device=dev)
+    sh = torch.empty(elems // ws, device=dev)
+    out = {}
+    for name in ("all_reduce", "reduce_scatter+all_gather"):
+        for it in range(reps + 1):
+            if it == 1:  # first call warms the communicator's buffers
+                _sync(ws)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            if name == "all_reduce":
+                dist.all_reduce(x)
+            else:
+                dist.reduce_scatter_tensor(sh, x)
+                dist.all_gather_into_tensor(x, sh)
+        e1.record()
+        e1.synchronize()
+        ms = _max_over_ranks(e0.elapsed_time(e1) / reps, dev, ws)
+        bus = 2.0 * (ws - 1) / ws * 4 * elems
+        out[name] = {"ms": round(ms, 4), "busbw_GBs": round(bus / (ms * 1e-3) / 1e9, 1)}
+    out["bytes"] = 4 * elems
+    return out
+
+
 def xgmi_link_probe(dev, ws, rank, reps=5, mib=256):
     """Peer read rates through IPC-mapped buffers (what the 153 GB/s per link
     means): every rank at once reads `mib` MiB from its ring neighbour (one direction of one
@@ -822,6 +851,18 @@ def main():
                     cap)
                 leg(f"{es.name}_int8_wire", run_q8, es, dev, ws, rank, ks, 1, cap)  # §8f row 4
         if ws > 1:
+            # RCCL's own all-reduce rate on the headline's bytes (the exchange's yardstick)
+            ref = leg("rccl_allreduce_ref", rccl_reference, dev, ws, rank,
+                      main_res["padded"] // (64 * ws) * (64 * ws), brief=False)
+            if isinstance(ref, dict) and "all_reduce" in ref:
+                bw = main_res["roofline"]["bus_bytes_per_step"] / (main_res["ms_per_step"] * 1e-3) / 1e9
+                em.line["exchange_efficiency"] = {
+                    "step_busbw_GBs": round(bw, 1),
+                    "rccl_allreduce_busbw_GBs": ref["all_reduce"]["busbw_GBs"],
+                    "frac_of_rccl_allreduce": round(bw / ref["all_reduce"]["busbw_GBs"], 4),
+                    "note": "whole outer step (kernels + collectives) as bus bytes / step time, "
+                            "over RCCL's all_reduce of the same bytes",
+                }
             # the replicated variant (all-reduce -> SGD on every peer) beside the sharded headline
             leg(f"{spec.name}_allreduce_variant", run_tree, spec, dev, ws, rank, a.steps,
                 a.warmup, wire, cap, False, False, False)
