@@ -76,13 +76,14 @@ def setup_dist(n_gpus):
     return ws, rank, dev
 
 
-def build(spec, dev, rank, wire, cap, fuse=False, shard=None, exchange="rccl", tile=None):
+def build(spec, dev, rank, wire, cap, fuse=False, shard=None, exchange="rccl", tile=None,
+          group=None):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree_device(spec, dev)
     params = [t.view(s) for t, s in zip(theta0, shapes)]
     eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=wire,
                     bucket_cap_elems=cap, fuse_single=fuse, shard=shard, exchange=exchange,
-                    **({} if tile is None else {"tile_chunks": tile}))
+                    group=group, **({} if tile is None else {"tile_chunks": tile}))
     # inner = θ_0 + this rank's noise (stands in for H inner steps)
     synth.inner_tree_device([p.view(-1) for p in params], 1, rank, out=[p.view(-1) for p in params])
     return eng
@@ -267,6 +268,32 @@ def parity_check(dev, ws, rank, wire):
     return {"tree": "tiny", "buckets": nb, "wire": "f32" if wire == torch.float32 else "bf16",
             "avg_delta_normwise_err": worst, "tolerance": tol,
             "replicas_identical": identical, "ok": bool(worst <= tol and identical)}
+
+
+def run_two_stages(spec, dev, ws, rank, steps, warmup, cap):
+    """The reference's two-stage SWARM layout (src/world.py:96-97, stage = rank % 2): two
+    disjoint DP groups of ws/2 ranks run their sharded outer steps at the same time, each over
+    its own RCCL communicator. value = ws · 4P / t_step (every rank steps a full
+    tree), max over all ranks."""
+    groups = [dist.new_group([r for r in range(ws) if r % 2 == s]) for s in range(2)]
+    g = groups[rank % 2]
+    eng = build(spec, dev, rank, torch.float32, cap, group=g)
+    for _ in range(max(warmup, 1)):
+        eng.step()
+    _sync(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step()
+    _sync(ws)
+    dt = _max_over_ranks(time.perf_counter() - t0, dev, ws)
+    res = {"tree": spec.name, "stages": 2, "dp_per_stage": ws // 2,
+           "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * spec.total() / (dt / steps) / 1e9,
+           "variant": "reduce_scatter -> shard SGD -> all_gather" if eng.sharded
+           else "all_reduce -> replicated SGD"}
+    eng.close()
+    del eng
+    torch.cuda.empty_cache()
+    return res
 
 
 def rccl_reference(dev, ws, rank, elems, reps=5):
@@ -871,6 +898,9 @@ def main():
                 wire, 16 << 20, False, False)
             leg(f"{spec.name}_dp_grad_sync", gradsync_rate, spec, dev, ws, rank,
                 max(3, a.steps // 2), brief=False)
+            if ws >= 4 and ws % 2 == 0:  # two concurrent disjoint DP groups (S = 2)
+                leg(f"{spec.name}_two_stages", run_two_stages, spec, dev, ws, rank, a.steps,
+                    a.warmup, cap, brief=False)
         if not a.no_parity:
             leg("f32", parity_check, dev, ws, rank, torch.float32, into=parity, brief=False)
             leg("bf16", parity_check, dev, ws, rank, torch.bfloat16, into=parity, brief=False)
