@@ -340,12 +340,14 @@ def xgmi_link_probe(dev, ws, rank, reps=5, mib=256):
     buf = torch.empty(n, device=dev)
     synth.fill_device(buf, 3, rank, 0.0, 1.0)
     dst = torch.empty(max(1, ws - 1) * n, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.call("dl_sys_fence", stream)  # the filled bytes leave this GPU's L2 before peers read
     pm = PeerMap({"buf": buf}, None, dev)
     if not pm.ok:
         return {"ok": False, "error": pm.reason}
+    _lib.call("dl_sys_fence", stream)  # no stale copies of peers' lines in this GPU's L2
     tab = pm.table("buf")
     p64 = ctypes.POINTER(ctypes.c_uint64)
-    stream = torch.cuda.current_stream(dev).cuda_stream
 
     def timed(srcs):
         arr = np.asarray(srcs, dtype=np.uint64)
@@ -733,6 +735,56 @@ def _brief(r):
     return {k: r[k] for k in keep if k in r}
 
 
+def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too):
+    """The legs that map peers' memory (the direct exchange, its parity check, the link
+    probe). Run by the isolated child processes below."""
+    extra, parity = {}, {}
+    r = _guard(run_tree, spec, dev, ws, rank, steps, warmup, torch.float32, cap, False, False,
+               None, "xgmi")
+    extra[f"{spec.name}_xgmi_exchange"] = _brief(r) if "value" in r else r
+    log(f"xgmi exchange leg done (rank {rank})")
+    if parity_too:
+        parity["xgmi"] = _guard(parity_xgmi, dev, ws, rank)
+    extra["xgmi_link_probe"] = _guard(xgmi_link_probe, dev, ws, rank)
+    return {"extra": extra, "parity": parity}
+
+
+def isolated_peer_access_legs(a, dev, ws, rank, timeout_s):
+    """Run peer_access_legs in a child process per rank (their own process group on a fresh
+    rendezvous port), so that a GPU fault or an abort while peers' memory is mapped ends the
+    children, not this run: the parents wait (bounded), then carry on to print the line.
+    Returns rank 0's child result, or an error record."""
+    port = [0]
+    if rank == 0:
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port[0] = sk.getsockname()[1]
+    dist.broadcast_object_list(port, src=0)
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"dl_bench_child_{port[0]}_{rank}.json")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port[0]))
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(ws), "--steps", str(a.steps),
+           "--warmup", str(a.warmup), "--tree", a.tree, "--bucket-mb", str(a.bucket_mb),
+           "--deadline", str(max(30.0, timeout_s - 10)), "--child-legs", "peer",
+           "--child-out", out] + (["--no-parity"] if a.no_parity else [])
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    try:
+        rc = subprocess.run(cmd, env=env, timeout=timeout_s, stdout=sys.stderr).returncode
+    except subprocess.TimeoutExpired:
+        rc = "timeout"
+    res = {"ok": False, "error": f"child exit {rc}"}
+    if rc == 0 and rank == 0 and os.path.exists(out):
+        with open(out) as f:
+            res = json.load(f)
+    if os.path.exists(out):
+        os.remove(out)
+    _sync(ws)  # every parent is past its child before anyone moves on
+    return res
+
+
 class _Emitter:
     """The one JSON line, assembled as the legs finish, printed exactly once by rank 0.
 
@@ -800,7 +852,25 @@ def main():
                     default=float(os.environ.get("DILOCO_BENCH_DEADLINE_S", "420")),
                     help="hard wall-clock bound of the whole run (s); side legs stop starting "
                          "at 70 %% of it")
+    ap.add_argument("--child-legs", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
+
+    if a.child_legs:  # one isolated child of isolated_peer_access_legs
+        ws, rank, dev = setup_dist(a.gpus)
+        threading_timer = _Emitter(rank, a.deadline)  # bounds the child too
+        _lib.load()
+        r = peer_access_legs(get_tree(a.tree), dev, ws, rank, a.steps, a.warmup,
+                             (a.bucket_mb << 20) // 4, not a.no_parity)
+        if rank == 0:
+            with open(a.child_out, "w") as f:
+                json.dump(r, f)
+        threading_timer.done = True
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+        threading_timer.timer.cancel()
+        return
 
     em = _Emitter(int(os.environ.get("RANK", "0")), a.deadline)
     soft = 0.7 * a.deadline
@@ -919,12 +989,20 @@ def main():
             log("timing the CPU baseline")
             em.line["cpu_baseline"] = cpu_baseline(spec)
         if ws > 1 and not a.no_xgmi:
-            # last: the direct peer-access exchange (IPC-mapped wires / θ, one fused kernel)
-            leg(f"{spec.name}_xgmi_exchange", run_tree, spec, dev, ws, rank, a.steps,
-                a.warmup, torch.float32, cap, False, False, None, "xgmi")
-            if not a.no_parity:
-                leg("xgmi", parity_xgmi, dev, ws, rank, into=parity, brief=False)
-            leg("xgmi_link_probe", xgmi_link_probe, dev, ws, rank, brief=False)
+            # last, in child processes: the direct peer-access exchange (IPC-mapped wires / θ,
+            # one fused kernel), its parity check and the link probe
+            left = a.deadline - _max_over_ranks(em.elapsed(), dev, ws) - 15
+            if left < 60:
+                em.skipped.append("peer_access_legs")
+            else:
+                em.running = "peer_access_legs (child processes)"
+                r = isolated_peer_access_legs(a, dev, ws, rank, min(240.0, left))
+                if "extra" in r:
+                    extra.update(r["extra"])
+                    parity.update(r["parity"])
+                else:
+                    extra["peer_access_legs"] = r
+                log(f"peer_access_legs done at {em.elapsed():.1f} s")
     em.running = "teardown"
     em.line["wall_s"] = round(em.elapsed(), 1)
     em.emit()

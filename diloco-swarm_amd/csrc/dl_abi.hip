@@ -501,6 +501,11 @@ DL_API int dl_enable_peer_access(int32_t peer) {
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_enable_peer_access");
 }
 
+DL_API int dl_sys_fence(dl_stream_t s) {
+  hipError_t e = dl::launch_sys_fence(static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_sys_fence");
+}
+
 DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each, void* dst,
                           dl_stream_t s) {
   if (!srcs || !dst) return fail(DL_E_ARG, "dl_peer_gather: null argument");

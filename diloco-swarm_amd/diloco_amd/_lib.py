@@ -81,6 +81,7 @@ SIGNATURES = {
     "dl_ipc_close": (ctypes.c_int, [_vp]),
     "dl_can_access_peer": (ctypes.c_int, [_i32, _i32, _pi32]),
     "dl_enable_peer_access": (ctypes.c_int, [_i32]),
+    "dl_sys_fence": (ctypes.c_int, [_vp]),
     "dl_peer_gather": (ctypes.c_int, [_pu64, _i32, _i64, _vp, _vp]),
     "dl_xgmi_reduce_sgd": (
         ctypes.c_int,

@@ -96,6 +96,10 @@ class HipKernels:
                   float(momentum), int(nesterov), int(first),
                   torch.cuda.current_stream(device).cuda_stream)
 
+    def sys_fence(self, device=None) -> None:
+        """L2 write-back + invalidate on every XCD (cross-GPU ordering of IPC-shared buffers)."""
+        _lib.call("dl_sys_fence", torch.cuda.current_stream(device).cuda_stream)
+
     # int8 wire codec (DL_Q8_SLOT_BYTES slots, one per chunk)
     def delta_q8(self, tree, bucket, inner_slot, theta, slots) -> None:
         _lib.call("dl_delta_q8", tree.handle, bucket, inner_slot, theta.data_ptr(),

@@ -412,12 +412,18 @@ class OuterSync:
         """delta_pack -> barrier -> dl_xgmi_reduce_sgd (peers' wires summed in rank order, SGD
         on this rank's shard, θ shard stored into every peer) -> barrier -> inner = θ."""
         self.pseudo_gradient(ALL)
+        # every XCD's L2 written back / invalidated around each barrier (dl_sys_fence): peers
+        # read this wire and write this θ over xGMI, outside this GPU's L2
+        self.k.sys_fence(self.device)
         self._barrier()
+        self.k.sys_fence(self.device)
         self.k.xgmi_reduce_sgd(self.peers.table("wire"), self.peers.table("theta"),
                                self.world_size, self.rank, self.x_lo, self.x_len, self.mom_x,
                                self.lr, self.momentum, self.nesterov, self.steps_done == 0,
                                self.device)
+        self.k.sys_fence(self.device)
         self._barrier()
+        self.k.sys_fence(self.device)
         self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
         self.k.scatter(self.tree, ALL, self.theta, SLOT_INNER)
 

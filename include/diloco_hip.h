@@ -244,6 +244,12 @@ DL_API int dl_ipc_close(void* base);
 DL_API int dl_can_access_peer(int32_t device, int32_t peer, int32_t* can);
 /* hipDeviceEnablePeerAccess(peer) from the current device; already enabled is success */
 DL_API int dl_enable_peer_access(int32_t peer);
+/* Stream-ordered system-scope fence on every XCD of this GPU (L2 write-back + invalidate):
+ * issue it after kernels whose stores peers will read over xGMI (before the barrier that
+ * releases the peers), and after that barrier before reading what peers wrote here or
+ * re-reading their memory. Coarse-grained (hipMalloc / PyTorch) buffers are otherwise
+ * coherent across GPUs only at the runtime's own synchronisation points. */
+DL_API int dl_sys_fence(dl_stream_t stream);
 /* link probe: dst[i*bytes_each ...] <- srcs[i][0 .. bytes_each) for i < nsrc (<= 8), all
  * sources streamed at once by one kernel (measures per-link and aggregate peer read rates) */
 DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each, void* dst,

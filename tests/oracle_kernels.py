@@ -120,6 +120,9 @@ class OracleKernels:
     def _chunk_range(self, tree, bucket):
         return (0, len(tree.chunks)) if bucket == -1 else tree.bucket_chunks[bucket]
 
+    def sys_fence(self, device=None):
+        pass  # host memory: nothing to order
+
     def delta_q8(self, tree, bucket, inner_slot, theta, slots):
         c0, c1 = self._chunk_range(tree, bucket)
         th, q = _np(theta), _np(slots)
