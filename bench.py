@@ -653,7 +653,7 @@ def gradsync_rate(spec, dev, ws, rank, steps):
 def p2p_rate(spec, dev, ws, rank, steps):
     """Device p2p transport (src/comm.py:16-69): two stages (rank % 2),
     stage-0 rank r sends a framed (2, mbs, seq, n_embd) activation to r+1 and gets it back;
-    header over gloo, payload over RCCL data groups. Opt-in (--p2p)."""
+    header over gloo, payload over RCCL data groups (isolated child legs, even N)."""
     from diloco_amd.p2p import DeviceRecvThread, DeviceSendThread, boundary_data_groups
     from diloco_amd.world import World
 
@@ -735,18 +735,26 @@ def _brief(r):
     return {k: r[k] for k in keep if k in r}
 
 
-def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too):
-    """The legs that map peers' memory (the direct exchange, its parity check, the link
-    probe). Run by the isolated child processes below."""
-    extra, parity = {}, {}
+def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too, dump=None):
+    """The legs that map peers' memory or run point-to-point traffic between GPUs: the direct
+    exchange, its parity check, the link probe and the device p2p transport (even N). Run by
+    the isolated child processes below; `dump(result)` is called after every leg so that a
+    child stopped by its watchdog still reports what it finished."""
+    res = {"extra": {}, "parity": {}}
+    dump = dump or (lambda r: None)
     r = _guard(run_tree, spec, dev, ws, rank, steps, warmup, torch.float32, cap, False, False,
                None, "xgmi")
-    extra[f"{spec.name}_xgmi_exchange"] = _brief(r) if "value" in r else r
-    log(f"xgmi exchange leg done (rank {rank})")
+    res["extra"][f"{spec.name}_xgmi_exchange"] = _brief(r) if "value" in r else r
+    dump(res)
     if parity_too:
-        parity["xgmi"] = _guard(parity_xgmi, dev, ws, rank)
-    extra["xgmi_link_probe"] = _guard(xgmi_link_probe, dev, ws, rank)
-    return {"extra": extra, "parity": parity}
+        res["parity"]["xgmi"] = _guard(parity_xgmi, dev, ws, rank)
+        dump(res)
+    res["extra"]["xgmi_link_probe"] = _guard(xgmi_link_probe, dev, ws, rank)
+    dump(res)
+    if ws % 2 == 0:  # SURVEY §8f row 3: header over gloo, framed payload over RCCL
+        res["extra"]["p2p_device_transport"] = _guard(p2p_rate, spec, dev, ws, rank, 10)
+        dump(res)
+    return res
 
 
 def isolated_peer_access_legs(a, dev, ws, rank, timeout_s):
@@ -776,9 +784,13 @@ def isolated_peer_access_legs(a, dev, ws, rank, timeout_s):
     except subprocess.TimeoutExpired:
         rc = "timeout"
     res = {"ok": False, "error": f"child exit {rc}"}
-    if rc == 0 and rank == 0 and os.path.exists(out):
-        with open(out) as f:
-            res = json.load(f)
+    if rank == 0 and os.path.exists(out):
+        try:
+            with open(out) as f:
+                res = json.load(f)  # what the children finished, even if they were stopped
+            res["child_exit"] = rc
+        except ValueError as e:
+            res = {"ok": False, "error": f"child exit {rc}; unreadable result: {e!r}"}
     if os.path.exists(out):
         os.remove(out)
     _sync(ws)  # every parent is past its child before anyone moves on
@@ -841,9 +853,11 @@ def main():
     ap.add_argument("--no-dropin", action="store_true", help="skip the host-outer-model rate")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-xgmi", action="store_true",
-                    help="skip the direct peer-access exchange legs at N > 1")
+                    help="skip the isolated legs at N > 1 (direct peer-access exchange, link "
+                         "probe, device p2p transport)")
     ap.add_argument("--p2p", action="store_true",
-                    help="also time the device p2p transport (N even; SURVEY §8f row 3)")
+                    help="(kept for compatibility: the device p2p transport is timed at every "
+                         "even N > 1, in the isolated child legs)")
     ap.add_argument("--only-headline", action="store_true",
                     help="headline tree only (for rocprofv3 runs of the same kernels)")
     ap.add_argument("--no-b2b", action="store_true",
@@ -860,11 +874,16 @@ def main():
         ws, rank, dev = setup_dist(a.gpus)
         threading_timer = _Emitter(rank, a.deadline)  # bounds the child too
         _lib.load()
-        r = peer_access_legs(get_tree(a.tree), dev, ws, rank, a.steps, a.warmup,
-                             (a.bucket_mb << 20) // 4, not a.no_parity)
-        if rank == 0:
-            with open(a.child_out, "w") as f:
-                json.dump(r, f)
+
+        def dump(r):
+            if rank == 0:
+                tmp = a.child_out + ".tmp"
+                with open(tmp, "w") as f:
+                    json.dump(r, f)
+                os.replace(tmp, a.child_out)
+
+        peer_access_legs(get_tree(a.tree), dev, ws, rank, a.steps, a.warmup,
+                         (a.bucket_mb << 20) // 4, not a.no_parity, dump)
         threading_timer.done = True
         if dist.is_initialized():
             dist.barrier()
@@ -976,8 +995,6 @@ def main():
             leg("bf16", parity_check, dev, ws, rank, torch.bfloat16, into=parity, brief=False)
             leg("int8", parity_q8, dev, ws, rank, into=parity, brief=False)
             leg("sharded", parity_sharded, dev, ws, rank, into=parity, brief=False)
-        if a.p2p:
-            leg("p2p_device_transport", p2p_rate, spec, dev, ws, rank, 10, brief=False)
         if not a.no_dropin:
             em.line["dropin_pcie"] = leg("dropin_pcie", dropin_rate, spec, dev, ws, rank, 5,
                                          into={}, brief=False)

@@ -46,15 +46,20 @@ class World:
                                     world_size=self.world_size)
         else:
             self.store = None
-        pairs = {(s, s + 1): dist.new_group(self.stage2ranks[s] + self.stage2ranks[s + 1])
+        # the reference's groups are gloo (its default group is, src/world.py:32-40); say so
+        # explicitly, so that a default RCCL group (benches) still gets host-side gloo groups
+        # for the p2p headers (any-source receives) and sync_outputs' object all-gather
+        pairs = {(s, s + 1): dist.new_group(self.stage2ranks[s] + self.stage2ranks[s + 1],
+                                            backend="gloo")
                  for s in range(self.num_stages - 1)}
         self.local_pg = pairs
         self.prev_stage_group = pairs.get((self.stage - 1, self.stage))
         self.next_stage_group = pairs.get((self.stage, self.stage + 1))
-        self.curr_stage_group = dist.new_group(self.stage2ranks[self.stage],
+        self.curr_stage_group = dist.new_group(self.stage2ranks[self.stage], backend="gloo",
                                                use_local_synchronization=True)
         fl = sorted(set(self.stage2ranks[0] + self.stage2ranks[self.num_stages - 1]))
-        self.first_last_stage_group = dist.new_group(fl, use_local_synchronization=True)
+        self.first_last_stage_group = dist.new_group(fl, backend="gloo",
+                                                     use_local_synchronization=True)
         dist.barrier()
 
     @classmethod
