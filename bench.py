@@ -757,11 +757,34 @@ def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too, dump=N
     return res
 
 
-def isolated_peer_access_legs(a, dev, ws, rank, timeout_s):
-    """Run peer_access_legs in a child process per rank (their own process group on a fresh
-    rendezvous port), so that a GPU fault or an abort while peers' memory is mapped ends the
-    children, not this run: the parents wait (bounded), then carry on to print the line.
-    Returns rank 0's child result, or an error record."""
+# RCCL settings tried beside the defaults at N > 1 (channel count and protocol are
+# the knobs for the xGMI all-reduce target); each runs in its own child process group
+RCCL_ENV_VARIANTS = {"min_channels_64": {"NCCL_MIN_NCHANNELS": "64"},
+                     "proto_simple": {"NCCL_PROTO": "Simple"}}
+
+
+def rccl_env_legs(spec, dev, ws, rank, steps, warmup, cap, dump=None):
+    """Under the child's RCCL environment: RCCL's own all_reduce / reduce_scatter+all_gather
+    rate on the headline's bytes and the headline's sharded outer step."""
+    res = {"env": {k: os.environ[k] for k in ("NCCL_MIN_NCHANNELS", "NCCL_PROTO",
+                                              "NCCL_ALGO") if k in os.environ}}
+    dump = dump or (lambda r: None)
+    res["rccl_allreduce_ref"] = _guard(rccl_reference, dev, ws, rank,
+                                       spec.total() // (64 * ws) * (64 * ws))
+    dump(res)
+    r = _guard(run_tree, spec, dev, ws, rank, steps, warmup, torch.float32, cap, False, False)
+    res["sharded_step"] = _brief(r) if "value" in r else r
+    dump(res)
+    return res
+
+
+def isolated_legs(a, dev, ws, rank, timeout_s, which="peer", extra_env=None):
+    """Run a set of legs in a child process per rank (their own process group on a fresh
+    rendezvous port): which="peer" -> peer_access_legs, so that a GPU fault or an abort while
+    peers' memory is mapped ends the children, not this run; which="rccl_env" ->
+    rccl_env_legs under `extra_env` (RCCL settings are read once per process). The parents
+    wait (bounded), then carry on to print the line. Returns rank 0's child result, or an
+    error record."""
     port = [0]
     if rank == 0:
         import socket
@@ -772,10 +795,10 @@ def isolated_peer_access_legs(a, dev, ws, rank, timeout_s):
     dist.broadcast_object_list(port, src=0)
     out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"dl_bench_child_{port[0]}_{rank}.json")
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
-    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port[0]))
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port[0]), **(extra_env or {}))
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(ws), "--steps", str(a.steps),
            "--warmup", str(a.warmup), "--tree", a.tree, "--bucket-mb", str(a.bucket_mb),
-           "--deadline", str(max(30.0, timeout_s - 10)), "--child-legs", "peer",
+           "--deadline", str(max(30.0, timeout_s - 10)), "--child-legs", which,
            "--child-out", out] + (["--no-parity"] if a.no_parity else [])
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -870,7 +893,7 @@ def main():
     ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
 
-    if a.child_legs:  # one isolated child of isolated_peer_access_legs
+    if a.child_legs:  # one isolated child of isolated_legs
         ws, rank, dev = setup_dist(a.gpus)
         threading_timer = _Emitter(rank, a.deadline)  # bounds the child too
         _lib.load()
@@ -882,8 +905,11 @@ def main():
                     json.dump(r, f)
                 os.replace(tmp, a.child_out)
 
-        peer_access_legs(get_tree(a.tree), dev, ws, rank, a.steps, a.warmup,
-                         (a.bucket_mb << 20) // 4, not a.no_parity, dump)
+        args = (get_tree(a.tree), dev, ws, rank, a.steps, a.warmup, (a.bucket_mb << 20) // 4)
+        if a.child_legs == "peer":
+            peer_access_legs(*args, not a.no_parity, dump)
+        else:
+            rccl_env_legs(*args, dump)
         threading_timer.done = True
         if dist.is_initialized():
             dist.barrier()
@@ -1013,13 +1039,22 @@ def main():
                 em.skipped.append("peer_access_legs")
             else:
                 em.running = "peer_access_legs (child processes)"
-                r = isolated_peer_access_legs(a, dev, ws, rank, min(240.0, left))
+                r = isolated_legs(a, dev, ws, rank, min(240.0, left))
                 if "extra" in r:
                     extra.update(r["extra"])
                     parity.update(r["parity"])
                 else:
                     extra["peer_access_legs"] = r
                 log(f"peer_access_legs done at {em.elapsed():.1f} s")
+            for name, env in RCCL_ENV_VARIANTS.items():
+                left = a.deadline - _max_over_ranks(em.elapsed(), dev, ws) - 15
+                if left < 60:
+                    em.skipped.append(f"rccl_env_{name}")
+                    continue
+                em.running = f"rccl_env_{name} (child processes)"
+                extra[f"rccl_env_{name}"] = isolated_legs(a, dev, ws, rank, min(120.0, left),
+                                                          "rccl_env", env)
+                log(f"rccl_env_{name} done at {em.elapsed():.1f} s")
     em.running = "teardown"
     em.line["wall_s"] = round(em.elapsed(), 1)
     em.emit()
