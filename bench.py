@@ -7,12 +7,18 @@
 
 One step = one full outer step of src/train.py:261-269 over the whole synthetic tree on every
 rank, device-resident (θ_outer, momentum and the wire buffer live in HBM):
-    dl_delta_pack (wire = θ_outer - inner) -> [RCCL all_reduce(SUM) per bucket, pipelined]
-    -> dl_unpack_sgd (g = wire/n, Nesterov SGD, inner = θ_outer)
-The headline runs this two-kernel pipeline at every N (BASELINE config #2 at N=1: the
-delta+pack kernels, no RCCL); the one-pass single-replica kernel (dl_delta_sgd, OuterSync's
-default at one replica) is reported beside it. Same tree per rank at every N (weak scaling):
-value = N * 4 * params / t_step. Rank 0 prints ONE JSON line.
+    N = 1  dl_delta_pack (wire = θ_outer - inner) -> dl_unpack_sgd (Nesterov SGD, inner = θ)
+           (BASELINE config #2: the delta+pack kernels, no RCCL)
+    N > 1  dl_delta_pack -> RCCL reduce_scatter -> dl_shard_sgd (/n, SGD on this rank's 1/n)
+           -> RCCL all_gather(θ) -> dl_scatter to inner, bucketed and pipelined
+Same tree per rank at every N (weak scaling): value = N * 4 * params / t_step, max over ranks.
+Rank 0 prints ONE JSON line: the headline with its roofline kernel (HIP events, PMC traffic
+from profiles/) and the CPU baseline (N = 1), then side legs (other trees and wires, the
+one-pass kernel, parity self-checks, drop-in rates, and at N > 1 the replicated variant,
+RCCL's own all_reduce rate, the two-stage layout; last, in isolated child processes, the
+direct peer-access exchange, the link probe, the device p2p transport and RCCL setting
+variants). A watchdog bounds the run (--deadline): the line is printed whatever a side leg
+does.
 """
 from __future__ import annotations
 
