@@ -81,6 +81,11 @@ def test_device_entry_points_fail_loudly_without_gpu():
     with pytest.raises(_lib.DilocoHipError) as e:
         PackedTree([10, 20])
     assert "hip" in str(e.value).lower()
+    # kernel launches with no device: an error code, never a silent no-op
+    with pytest.raises(_lib.DilocoHipError):
+        _lib.call("dl_sys_fence", None)
+    with pytest.raises(_lib.DilocoHipError):
+        _lib.call("dl_shard_sgd", 16, _lib.DL_F32, 1, 32, 48, 4, 0.7, 0.9, 1, 0, None)
 
 
 def test_missing_library_is_an_import_error(tmp_path, monkeypatch):
