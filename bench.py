@@ -160,6 +160,8 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
            "wire": "bf16" if wire == torch.bfloat16 else "f32",
            "tile_chunks": eng.tile_chunks if single and not fuse else None,
            "variant": ("one replica: dl_delta_sgd (one pass)" if single and fuse
+                       else "direct exchange from the peers' inner arenas (dl_xgmi_delta_sgd)"
+                       if eng.xgmi_inner
                        else ("one replica: dl_delta_pack -> dl_unpack_sgd"
                              + (f", tiles of {eng.tile_chunks} chunks" if eng.tile_chunks
                                 else ", whole-range launches")) if single
@@ -385,12 +387,12 @@ def xgmi_link_probe(dev, ws, rank, reps=5, mib=256):
                     "one_peer = ring neighbour = one direction of one link", "ok": ok}
 
 
-def parity_xgmi(dev, ws, rank):
+def parity_xgmi(dev, ws, rank, exchange="xgmi"):
     """The direct exchange (exchange='xgmi') against the RCCL sharded step on the tiny tree,
     2 outer steps: θ and momentum normwise <= 1e-6 per tensor (bit-exact at n <= 2; the direct
     exchange sums in rank order, RCCL in its own order), inner == θ, replicas identical."""
     spec = get_tree("tiny")
-    ea = build(spec, dev, rank, torch.float32, 1 << 20, exchange="xgmi")
+    ea = build(spec, dev, rank, torch.float32, 1 << 20, exchange=exchange)
     eb = build(spec, dev, rank, torch.float32, 1 << 20)
     for s in (1, 2):
         for e in (ea, eb):
@@ -748,13 +750,14 @@ def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too, dump=N
     child stopped by its watchdog still reports what it finished."""
     res = {"extra": {}, "parity": {}}
     dump = dump or (lambda r: None)
-    r = _guard(run_tree, spec, dev, ws, rank, steps, warmup, torch.float32, cap, False, False,
-               None, "xgmi")
-    res["extra"][f"{spec.name}_xgmi_exchange"] = _brief(r) if "value" in r else r
-    dump(res)
-    if parity_too:
-        res["parity"]["xgmi"] = _guard(parity_xgmi, dev, ws, rank)
+    for ex in ("xgmi", "xgmi_inner"):  # peers' wires / peers' inner arenas (no pack pass)
+        r = _guard(run_tree, spec, dev, ws, rank, steps, warmup, torch.float32, cap, False,
+                   False, None, ex)
+        res["extra"][f"{spec.name}_{ex}_exchange"] = _brief(r) if "value" in r else r
         dump(res)
+        if parity_too:
+            res["parity"][ex] = _guard(parity_xgmi, dev, ws, rank, ex)
+            dump(res)
     res["extra"]["xgmi_link_probe"] = _guard(xgmi_link_probe, dev, ws, rank)
     dump(res)
     if ws % 2 == 0:  # SURVEY §8f row 3: header over gloo, framed payload over RCCL

@@ -525,31 +525,51 @@ DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_peer_gather");
 }
 
+}  // extern "C"
+
+namespace {
+int xgmi_step(const char* who, bool delta, const uint64_t* srcs, const uint64_t* thetas,
+              int32_t n, int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
+              float momentum, int32_t nesterov, int32_t first_step, dl_stream_t s) {
+  if (!srcs || !thetas) return fail(DL_E_ARG, "%s: null peer table", who);
+  if (n < 1 || n > dl::kMaxPeers || rank < 0 || rank >= n)
+    return fail(DL_E_ARG, "%s: rank %d of %d (1..%d peers)", who, rank, n, dl::kMaxPeers);
+  if (lo < 0 || len < 0 || lo % 4 || len % 4)
+    return fail(DL_E_ARG, "%s: shard [%lld, +%lld) not a multiple of 4", who, (long long)lo,
+                (long long)len);
+  if (momentum != 0.f) DL_TRY(check_packed(mom, who, "momentum"));
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "%s: Nesterov momentum requires a momentum", who);
+  dl::XgmiPeers p{};
+  for (int32_t q = 0; q < n; ++q) {
+    p.wire[q] = reinterpret_cast<const float*>(srcs[q]);
+    p.theta[q] = reinterpret_cast<float*>(thetas[q]);
+    DL_TRY(check_packed(p.wire[q], who, delta ? "inner" : "wire"));
+    DL_TRY(check_packed(p.theta[q], who, "theta"));
+  }
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_xgmi_reduce_sgd(p, n, rank, lo, len, mom, a, delta,
+                                            static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, who);
+}
+}  // namespace
+
+extern "C" {
+
 DL_API int dl_xgmi_reduce_sgd(const uint64_t* wires, const uint64_t* thetas, int32_t n,
                               int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
                               float momentum, int32_t nesterov, int32_t first_step,
                               dl_stream_t s) {
-  if (!wires || !thetas) return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: null peer table");
-  if (n < 1 || n > dl::kMaxPeers || rank < 0 || rank >= n)
-    return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: rank %d of %d (1..%d peers)", rank, n,
-                dl::kMaxPeers);
-  if (lo < 0 || len < 0 || lo % 4 || len % 4)
-    return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: shard [%lld, +%lld) not a multiple of 4",
-                (long long)lo, (long long)len);
-  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_xgmi_reduce_sgd", "momentum"));
-  if (nesterov && momentum == 0.f)
-    return fail(DL_E_ARG, "dl_xgmi_reduce_sgd: Nesterov momentum requires a momentum");
-  dl::XgmiPeers p{};
-  for (int32_t q = 0; q < n; ++q) {
-    p.wire[q] = reinterpret_cast<const float*>(wires[q]);
-    p.theta[q] = reinterpret_cast<float*>(thetas[q]);
-    DL_TRY(check_packed(p.wire[q], "dl_xgmi_reduce_sgd", "wire"));
-    DL_TRY(check_packed(p.theta[q], "dl_xgmi_reduce_sgd", "theta"));
-  }
-  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
-  hipError_t e = dl::launch_xgmi_reduce_sgd(p, n, rank, lo, len, mom, a,
-                                            static_cast<hipStream_t>(s));
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_xgmi_reduce_sgd");
+  return xgmi_step("dl_xgmi_reduce_sgd", false, wires, thetas, n, rank, lo, len, mom, lr,
+                   momentum, nesterov, first_step, s);
+}
+
+DL_API int dl_xgmi_delta_sgd(const uint64_t* inners, const uint64_t* thetas, int32_t n,
+                             int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
+                             float momentum, int32_t nesterov, int32_t first_step,
+                             dl_stream_t s) {
+  return xgmi_step("dl_xgmi_delta_sgd", true, inners, thetas, n, rank, lo, len, mom, lr,
+                   momentum, nesterov, first_step, s);
 }
 
 DL_API int dl_delta_q8(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,

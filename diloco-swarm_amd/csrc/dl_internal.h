@@ -47,8 +47,9 @@ struct XgmiPeers {
   const float* wire[kMaxPeers];
   float* theta[kMaxPeers];
 };
+// delta: p.wire[] holds the peers' packed inner parameters (dl_xgmi_delta_sgd)
 hipError_t launch_xgmi_reduce_sgd(const XgmiPeers& p, int32_t n, int32_t rank, int64_t lo,
-                                  int64_t len, float* mom, SgdArgs a, hipStream_t s);
+                                  int64_t len, float* mom, SgdArgs a, bool delta, hipStream_t s);
 hipError_t launch_sys_fence(hipStream_t s);
 hipError_t launch_peer_gather(const XgmiPeers& p, int32_t nsrc, int32_t each4, float* dst,
                               hipStream_t s);

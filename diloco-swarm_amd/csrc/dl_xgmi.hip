@@ -17,7 +17,12 @@ namespace {
 constexpr int kXU = 2;                          // float4 per lane per stream
 constexpr int kXChunk = kThreads * kXU * 4;     // 2048 elements per workgroup
 
-template <int N>
+// DELTA = false: p.wire[q] is rank q's packed pseudo-gradient (dl_delta_pack's wire).
+// DELTA = true (dl_xgmi_delta_sgd): p.wire[q] is rank q's packed INNER parameters and the
+// kernel forms the pseudo-gradient itself, θ_outer - inner_q -- the same single subtraction
+// rank q would have made (src/utils.py:221; θ_outer is identical on every replica), so the
+// result is bit-identical and no rank runs dl_delta_pack.
+template <int N, bool DELTA>
 __global__ void __launch_bounds__(kThreads)
     k_xgmi_reduce_sgd(XgmiPeers p, int32_t rank, int64_t lo, int64_t len, float* __restrict__ mom,
                       SgdArgs a, int32_t mode) {
@@ -40,10 +45,12 @@ __global__ void __launch_bounds__(kThreads)
     for (int u = 0; u < kXU; ++u) {
       const int64_t e = base + int64_t(u * kThreads + threadIdx.x) * 4;
       if (e < len) {
-        float4 g = w[0][u];
+        float4 g = DELTA ? sub4(t[u], w[0][u]) : w[0][u];
 #pragma unroll
-        for (int q = 1; q < N; ++q)
-          g = make_float4(g.x + w[q][u].x, g.y + w[q][u].y, g.z + w[q][u].z, g.w + w[q][u].w);
+        for (int q = 1; q < N; ++q) {
+          const float4 d = DELTA ? sub4(t[u], w[q][u]) : w[q][u];
+          g = make_float4(g.x + d.x, g.y + d.y, g.z + d.z, g.w + d.w);
+        }
         if (N > 1) g = div4(g, float(N));
         if (mode == 0) {
           sgd1<0>(g.x, m[u].x, t[u].x, a);
@@ -74,12 +81,16 @@ __global__ void __launch_bounds__(kThreads)
 
 template <int N>
 hipError_t launch_n(const XgmiPeers& p, int32_t rank, int64_t lo, int64_t len, float* mom,
-                    SgdArgs a, hipStream_t s) {
+                    SgdArgs a, bool delta, hipStream_t s) {
   const int32_t mode = a.momentum == 0.f ? 0 : (a.first ? 1 : 2);
   const int64_t blocks = (len + kXChunk - 1) / kXChunk;
   const int32_t grid = int32_t(blocks < 65536 ? blocks : 65536);
-  hipLaunchKernelGGL(k_xgmi_reduce_sgd<N>, dim3(grid), dim3(kThreads), 0, s, p, rank, lo, len, mom,
-                     a, mode);
+  if (delta)
+    hipLaunchKernelGGL((k_xgmi_reduce_sgd<N, true>), dim3(grid), dim3(kThreads), 0, s, p, rank,
+                       lo, len, mom, a, mode);
+  else
+    hipLaunchKernelGGL((k_xgmi_reduce_sgd<N, false>), dim3(grid), dim3(kThreads), 0, s, p, rank,
+                       lo, len, mom, a, mode);
   return hipGetLastError();
 }
 
@@ -133,17 +144,17 @@ hipError_t launch_peer_gather(const XgmiPeers& p, int32_t nsrc, int32_t each4, f
 }
 
 hipError_t launch_xgmi_reduce_sgd(const XgmiPeers& p, int32_t n, int32_t rank, int64_t lo,
-                                  int64_t len, float* mom, SgdArgs a, hipStream_t s) {
+                                  int64_t len, float* mom, SgdArgs a, bool delta, hipStream_t s) {
   if (len <= 0) return hipSuccess;
   switch (n) {
-    case 1: return launch_n<1>(p, rank, lo, len, mom, a, s);
-    case 2: return launch_n<2>(p, rank, lo, len, mom, a, s);
-    case 3: return launch_n<3>(p, rank, lo, len, mom, a, s);
-    case 4: return launch_n<4>(p, rank, lo, len, mom, a, s);
-    case 5: return launch_n<5>(p, rank, lo, len, mom, a, s);
-    case 6: return launch_n<6>(p, rank, lo, len, mom, a, s);
-    case 7: return launch_n<7>(p, rank, lo, len, mom, a, s);
-    case 8: return launch_n<8>(p, rank, lo, len, mom, a, s);
+    case 1: return launch_n<1>(p, rank, lo, len, mom, a, delta, s);
+    case 2: return launch_n<2>(p, rank, lo, len, mom, a, delta, s);
+    case 3: return launch_n<3>(p, rank, lo, len, mom, a, delta, s);
+    case 4: return launch_n<4>(p, rank, lo, len, mom, a, delta, s);
+    case 5: return launch_n<5>(p, rank, lo, len, mom, a, delta, s);
+    case 6: return launch_n<6>(p, rank, lo, len, mom, a, delta, s);
+    case 7: return launch_n<7>(p, rank, lo, len, mom, a, delta, s);
+    case 8: return launch_n<8>(p, rank, lo, len, mom, a, delta, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -87,6 +87,10 @@ SIGNATURES = {
         ctypes.c_int,
         [_pu64, _pu64, _i32, _i32, _i64, _i64, _vp, _f32, _f32, _i32, _i32, _vp],
     ),
+    "dl_xgmi_delta_sgd": (
+        ctypes.c_int,
+        [_pu64, _pu64, _i32, _i32, _i64, _i64, _vp, _f32, _f32, _i32, _i32, _vp],
+    ),
     "dl_last_error": (ctypes.c_char_p, []),
     "dl_abi_version": (ctypes.c_int, []),
 }

@@ -96,6 +96,15 @@ class HipKernels:
                   float(momentum), int(nesterov), int(first),
                   torch.cuda.current_stream(device).cuda_stream)
 
+    def xgmi_delta_sgd(self, inners, thetas, n, rank, lo, length, mom, lr, momentum, nesterov,
+                       first, device=None) -> None:
+        """Direct exchange from the peers' packed inner arenas (no wire): g formed in-kernel."""
+        p64 = ctypes.POINTER(ctypes.c_uint64)
+        _lib.call("dl_xgmi_delta_sgd", inners.ctypes.data_as(p64), thetas.ctypes.data_as(p64),
+                  int(n), int(rank), int(lo), int(length), _ptr(mom), float(lr),
+                  float(momentum), int(nesterov), int(first),
+                  torch.cuda.current_stream(device).cuda_stream)
+
     def sys_fence(self, device=None) -> None:
         """L2 write-back + invalidate on every XCD (cross-GPU ordering of IPC-shared buffers)."""
         _lib.call("dl_sys_fence", torch.cuda.current_stream(device).cuda_stream)

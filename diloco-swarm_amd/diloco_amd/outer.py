@@ -17,7 +17,9 @@ Exchange variants, all bucketed and pipelined across buckets:
   replicated         (shard=False; the bf16 wire's default) RCCL all-reduce -> dl_unpack_sgd
                      (/n + SGD + copy-back, 24 B/param) on every replica
   int8 wire          dl_delta_q8 -> all_to_all -> dl_q8_reduce -> all_gather -> dl_unpack_sgd_q8
-  direct (xgmi)      exchange="xgmi": IPC-mapped peers, one dl_xgmi_reduce_sgd per rank
+  direct (xgmi)      exchange="xgmi": IPC-mapped peers, one dl_xgmi_reduce_sgd per rank;
+                     exchange="xgmi_inner": no wire -- the inner params live in one packed
+                     arena the peers read, dl_xgmi_delta_sgd forms θ - inner_q itself
 
 Layout in HBM: θ_outer, momentum and the wire are packed arrays in
 parameters() order with 256-B-aligned segments; the inner parameters stay where PyTorch
@@ -92,6 +94,7 @@ class OuterSync:
         exchange: str = "rccl",
         tile_chunks: int = DEFAULT_TILE_CHUNKS,
     ):
+        self._objs = list(params)  # the caller's objects (exchange="xgmi_inner" relays them)
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
                                            for p in params]
         if not self.params:
@@ -126,12 +129,16 @@ class OuterSync:
             shard = self.world_size > 1 and wire_dtype == torch.float32
         if shard and self.q8:
             raise ValueError("the int8 wire has its own exchange; shard=True needs f32/bf16")
-        if exchange not in ("rccl", "xgmi"):
-            raise ValueError(f"exchange {exchange!r}: 'rccl' or 'xgmi'")
+        if exchange not in ("rccl", "xgmi", "xgmi_inner"):
+            raise ValueError(f"exchange {exchange!r}: 'rccl', 'xgmi' or 'xgmi_inner'")
         # xgmi: the direct peer-access exchange (dl_xgmi_reduce_sgd) over IPC-mapped buffers
-        self.xgmi = exchange == "xgmi"
+        # xgmi_inner: the same with no wire -- the inner parameters move into one packed arena
+        # that the peers read, and the exchange kernel forms θ_outer - inner_q itself
+        # (dl_xgmi_delta_sgd): no dl_delta_pack pass, no wire buffer
+        self.xgmi = exchange in ("xgmi", "xgmi_inner")
+        self.xgmi_inner = exchange == "xgmi_inner"
         if self.xgmi and wire_dtype != torch.float32:
-            raise ValueError("exchange='xgmi' sends the fp32 wire")
+            raise ValueError(f"exchange={exchange!r} sends the fp32 wire")
         self.sharded = bool(shard) and not self.xgmi
         # sharded / xgmi: buckets (and the tree) align to 64·n elements -> n equal aligned shards
         balign = _lib.ALIGN_ELEMS * (self.world_size if (self.sharded or self.xgmi) else 1)
@@ -158,6 +165,8 @@ class OuterSync:
             self.q_slots = torch.zeros(base * Q8_SLOT, dtype=torch.uint8, **z)
             self.q_recv = torch.zeros(n * mmax * Q8_SLOT, dtype=torch.uint8, **z)
             self.q_red = torch.zeros(mmax * Q8_SLOT, dtype=torch.uint8, **z)
+        elif self.xgmi_inner:
+            self.wire = None
         else:
             self.wire = torch.zeros(self.tree.total, dtype=wire_dtype, **z)
         self.k.gather(self.tree, ALL, SLOT_INNER, self.theta)
@@ -186,7 +195,10 @@ class OuterSync:
             self.mom_x = (torch.zeros(self.x_len, dtype=torch.float32, **z)
                           if self.momentum != 0 else None)
             self._flag = torch.zeros(1, dtype=torch.float32, **z)
-            self.peers = PeerMap({"wire": self.wire, "theta": self.theta},
+            if self.xgmi_inner:
+                self._relay_inner()
+            src = self.inner_arena if self.xgmi_inner else self.wire
+            self.peers = PeerMap({"src": src, "theta": self.theta},
                                  group if n > 1 else None, self.device)
             if not self.peers.ok:
                 raise RuntimeError(f"exchange='xgmi' unavailable: {self.peers.reason}")
@@ -199,8 +211,27 @@ class OuterSync:
                        if side_stream and self.device.type == "cuda" else None)
 
     # ---- building blocks (each stream-ordered on the current stream) ----------------------
+    def _relay_inner(self) -> None:
+        """exchange="xgmi_inner": move every inner parameter's storage into one packed arena
+        (same layout as θ; values, Parameter objects, autograd and optimizer state unchanged),
+        so the peers map ONE allocation per rank and read the inner values directly."""
+        z = dict(dtype=torch.float32, device=self.device)
+        self.inner_arena = torch.zeros(self.tree.total, **z)
+        with torch.no_grad():
+            for i, o in enumerate(self._objs):
+                lo = int(self.tree.seg_off[i])
+                v = self.inner_arena[lo:lo + o.numel()].view(o.shape)
+                v.copy_(o.data if isinstance(o, torch.nn.Parameter) else o)
+                o.data = v
+        self.params = [o.data if isinstance(o, torch.nn.Parameter) else o for o in self._objs]
+        self._arena_ptrs = [o.data_ptr() for o in self._objs]
+        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+
     def pseudo_gradient(self, bucket: int = ALL) -> None:
         """wire[bucket] = θ_outer - inner (a2); int8 wire: its quantised slots."""
+        if self.xgmi_inner:
+            raise RuntimeError("exchange='xgmi_inner' has no wire: the exchange kernel forms "
+                               "the pseudo-gradient; use step()")
         self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
         if self.q8:
             self.k.delta_q8(self.tree, bucket, SLOT_INNER, self.theta, self.q8_region(bucket))
@@ -411,21 +442,30 @@ class OuterSync:
     def _step_xgmi(self) -> None:
         """delta_pack -> barrier -> dl_xgmi_reduce_sgd (peers' wires summed in rank order, SGD
         on this rank's shard, θ shard stored into every peer) -> barrier -> inner = θ."""
-        self.pseudo_gradient(ALL)
+        if self.xgmi_inner:
+            if any(o.data_ptr() != e for o, e in zip(self._objs, self._arena_ptrs)):
+                raise RuntimeError("exchange='xgmi_inner': an inner parameter's storage was "
+                                   "replaced after the engine moved it into its packed arena, "
+                                   "which the peers read")
+        else:
+            self.pseudo_gradient(ALL)
         # every XCD's L2 written back / invalidated around each barrier (dl_sys_fence): peers
-        # read this wire and write this θ over xGMI, outside this GPU's L2
+        # read this wire (or inner arena) and write this θ over xGMI, outside this GPU's L2
         self.k.sys_fence(self.device)
         self._barrier()
         self.k.sys_fence(self.device)
-        self.k.xgmi_reduce_sgd(self.peers.table("wire"), self.peers.table("theta"),
-                               self.world_size, self.rank, self.x_lo, self.x_len, self.mom_x,
-                               self.lr, self.momentum, self.nesterov, self.steps_done == 0,
-                               self.device)
+        step = self.k.xgmi_delta_sgd if self.xgmi_inner else self.k.xgmi_reduce_sgd
+        step(self.peers.table("src"), self.peers.table("theta"), self.world_size, self.rank,
+             self.x_lo, self.x_len, self.mom_x, self.lr, self.momentum, self.nesterov,
+             self.steps_done == 0, self.device)
         self.k.sys_fence(self.device)
         self._barrier()
         self.k.sys_fence(self.device)
-        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
-        self.k.scatter(self.tree, ALL, self.theta, SLOT_INNER)
+        if self.xgmi_inner:  # inner = θ: one flat copy of the arena (padding stays zero)
+            self.inner_arena.copy_(self.theta)
+        else:
+            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+            self.k.scatter(self.tree, ALL, self.theta, SLOT_INNER)
 
     def _step_q8(self, pipeline: bool) -> None:
         nb = self.tree.n_buckets

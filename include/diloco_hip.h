@@ -259,6 +259,17 @@ DL_API int dl_xgmi_reduce_sgd(const uint64_t* wires, const uint64_t* thetas, int
                               float momentum, int32_t nesterov, int32_t first_step,
                               dl_stream_t stream);
 
+/* dl_xgmi_reduce_sgd without a wire: inners[q] is rank q's INNER parameters laid out in the
+ * packed layout (OuterSync(exchange="xgmi_inner") keeps them in one such arena), and the
+ * kernel forms g = (Σ_q (thetas[rank][k] - inners[q][k]) in rank order) / n itself -- the
+ * subtraction of src/utils.py:221 rank q would have made, θ_outer being identical on every
+ * rank -- so no rank runs dl_delta_pack. Bit-identical to dl_delta_pack + dl_xgmi_reduce_sgd;
+ * same ordering rules (between two barriers, dl_sys_fence around each). */
+DL_API int dl_xgmi_delta_sgd(const uint64_t* inners, const uint64_t* thetas, int32_t n,
+                             int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
+                             float momentum, int32_t nesterov, int32_t first_step,
+                             dl_stream_t stream);
+
 DL_API const char* dl_last_error(void);
 DL_API int dl_abi_version(void);
 

@@ -189,7 +189,7 @@ def _worker(rank, world, port, mode, out):
             rec[f"theta_s{s}"] = _flat(eng.unpacked(eng.theta))
             rec[f"buf_s{s}"] = _flat(eng.unpacked(eng.momentum_full()))
             rec[f"inner_s{s}"] = _flat(params)
-    elif mode == "engine_xgmi":
+    elif mode in ("engine_xgmi", "engine_xgmi_inner"):
         # the direct exchange: wires and θ IPC-mapped between the processes (same GPU here),
         # one dl_xgmi_reduce_sgd per rank between two barriers
         from diloco_amd import synth
@@ -199,8 +199,12 @@ def _worker(rank, world, port, mode, out):
         spec = get_tree("micro")
         shapes = [s for _, s in spec.params()]
         params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
-        eng = OuterSync(params, world_size=world, bucket_cap_elems=4096, exchange="xgmi")
+        exchange = "xgmi" if mode == "engine_xgmi" else "xgmi_inner"
+        eng = OuterSync(params, world_size=world, bucket_cap_elems=4096, exchange=exchange)
         assert eng.xgmi and eng.tree.total % (64 * world) == 0
+        if exchange == "xgmi_inner":  # the params now live in the arena the peers read
+            base = eng.inner_arena.data_ptr()
+            assert all(base <= p.data_ptr() < base + 4 * eng.tree.total for p in params)
         for s in (1, 2):
             th = [t.reshape(-1) for t in eng.unpacked(eng.theta)]
             synth.inner_tree_device(th, s, rank, out=[p.view(-1) for p in params])
@@ -286,16 +290,18 @@ def test_two_peers_on_gpu_match_reference(mode):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
 
 
+@pytest.mark.parametrize("exchange", ["xgmi", "xgmi_inner"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_direct_exchange_between_processes(world):
-    """exchange='xgmi' with `world` processes on the one GPU (IPC between processes of one
-    device; across devices the same code reads over xGMI): every replica equals the oracle's
-    rank-order sum + SGD bit-exact at any n, and the reference bit-exact at n = 2."""
+def test_direct_exchange_between_processes(world, exchange):
+    """exchange='xgmi' (peers' wires) and 'xgmi_inner' (peers' inner arenas, no wire) with
+    `world` processes on the one GPU (IPC between processes of one device; across devices the
+    same code reads over xGMI): every replica equals the oracle's rank-order sum + SGD
+    bit-exact at any n, and the reference bit-exact at n = 2."""
     from diloco_amd import synth
     from diloco_amd.trees import get_tree
     from oracle import oracle
 
-    recs = _run("engine_xgmi", world)
+    recs = _run(f"engine_{exchange}", world)
     spec = get_tree("micro")
     st = oracle.OuterState(synth.outer_tree(spec.numels(), spec.init_spec()))
     for s in (1, 2):

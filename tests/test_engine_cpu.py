@@ -119,5 +119,14 @@ def test_direct_exchange_arguments():
         OuterSync(params, world_size=1, exchange="xgmi", wire_dtype=torch.bfloat16)
     e = OuterSync(params, world_size=1, exchange="xgmi")  # one rank: no peers to map
     assert e.xgmi and not e.sharded and e.peers.ok
+    # xgmi_inner: the inner parameters move into the engine's packed arena, values unchanged
+    before = [p.detach().clone() for p in params]
+    ei = OuterSync(params, world_size=1, exchange="xgmi_inner")
+    assert ei.xgmi and ei.xgmi_inner and ei.wire is None
+    base, nbytes = ei.inner_arena.data_ptr(), 4 * ei.tree.total
+    assert all(base <= p.data_ptr() < base + nbytes for p in params)
+    assert all(torch.equal(p, b) for p, b in zip(params, before))
+    with pytest.raises(RuntimeError, match="no wire"):
+        ei.pseudo_gradient()
     with pytest.raises(RuntimeError, match="exchange='xgmi'"):
         e.apply()

@@ -346,6 +346,34 @@ def test_tiled_pack_sgd_micro_matches_reference():
         assert np.concatenate(_host(params)).tobytes() == g[f"theta_s{s}"].tobytes()
 
 
+def test_direct_exchange_from_inner_arena_single_replica():
+    """exchange='xgmi_inner' at one replica: the inner parameters move into the engine's packed
+    arena (values unchanged), the outer steps equal the reference's (micro tree, n = 1), and a
+    parameter whose storage is replaced afterwards is refused."""
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    params = [t.clone().view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
+    before = [p.clone() for p in params]
+    e = OuterSync(params, world_size=1, exchange="xgmi_inner")
+    base = e.inner_arena.data_ptr()
+    assert all(base <= p.data_ptr() < base + 4 * e.tree.total for p in params)
+    assert all(torch.equal(p, b) for p, b in zip(params, before))
+    g = load_npz("micro_n1.npz")
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        e.step()
+        torch.cuda.synchronize()
+        assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert np.concatenate(_host(e.unpacked(e.momentum_full()))).tobytes() == \
+            g[f"buf_s{s}"].tobytes()
+        assert np.concatenate(_host(params)).tobytes() == g[f"theta_s{s}"].tobytes()
+    params[3].data = params[3].data.clone()
+    with pytest.raises(RuntimeError, match="storage was replaced"):
+        e.step()
+    e.close()
+
+
 def test_t13b_full_size_sampled_tensors_vs_oracle_and_fused():
     """BASELINE configs #4/#5 tree at full size (1.31 B params): the two-kernel path equals the
     one-pass kernel everywhere (size-independent property), and the largest (wte, 103 M),

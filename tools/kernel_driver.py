@@ -39,6 +39,11 @@ def main():
     for e in (q8, sh, xg):
         for _ in range(reps + 1):
             e.step()
+    # last: exchange="xgmi_inner" moves `params` into its own arena
+    xi = OuterSync(params, world_size=1, exchange="xgmi_inner")
+    for e in (xi,):
+        for _ in range(reps + 1):
+            e.step()
     torch.cuda.synchronize()
     print(f"kernel_driver: {tree} x{reps} done")
 

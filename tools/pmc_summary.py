@@ -21,6 +21,8 @@ def short(name):
              "k_q8_reduce": "q8_reduce", "DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd",
              "UnpackAvg": "unpack_avg", "DeltaSgd": "delta_sgd", "Gather": "gather",
              "Scatter": "scatter", "k_fill_synth": "fill_synth"}
+    if "k_xgmi_reduce_sgd" in name and ", true>" in name:
+        return "xgmi_delta_sgd"  # the pack-free variant (exchange="xgmi_inner")
     for k, v in names.items():
         if k in name:
             first = ((k in ("UnpackSgd", "k_flat") and ", 1>" in name)
