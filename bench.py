@@ -572,10 +572,14 @@ def parity_q8(dev, ws, rank):
             "replicas_identical": identical, "ok": bool(worst <= 1.0 and identical)}
 
 
-def dropin_rate(spec, dev, ws, rank, steps, placement="host"):
+def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync", inner_fn=None):
     """The reference's call sequence (src/train.py:261-269) through the drop-in functions.
     placement "host": the reference's host-resident outer model, PCIe transfers included
-    (DESIGN.md "Host-memory ends"); "device": the outer model in HBM."""
+    (DESIGN.md "Host-memory ends"); "device": the outer model in HBM.
+    write_back "deferred": the host placement's write-back DMAs issued by sync_inner_model
+    and not waited for. inner_fn: GPU work standing in for the inner steps that follow an
+    outer step in training, enqueued after it and inside the timed cycle (the reference
+    synchronises the device after every inner step, src/train.py:243)."""
     from types import SimpleNamespace
 
     from diloco_amd.comm import TrainingComm
@@ -592,7 +596,7 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host"):
     inner = torch.nn.Module()
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
-    outer = get_outer_model(inner, placement)
+    outer = get_outer_model(inner, placement, write_back=write_back)
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
@@ -609,6 +613,8 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host"):
         opt.step()
         t.append(time.perf_counter())
         sync_inner_model(outer, inner)
+        if inner_fn is not None:
+            inner_fn()
         torch.cuda.synchronize()
         t.append(time.perf_counter())
         if record:
@@ -623,14 +629,61 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host"):
         one(True)
     dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
     P = spec.total()
+    d2h = 0
+    if placement == "host":
+        d2h = (16 if ws > 1 and write_back == "sync" else 12) * P
+    if inner_fn is not None:
+        phases["inner_work_and_sync"] = phases.pop("sync_inner_model")
     return {"tree": spec.name, "value": round(ws * 4.0 * P / dt / 1e9, 2), "unit": "GB/s",
             "ms_per_step": round(dt * 1e3, 3),
             "phase_ms": {k: round(v / steps * 1e3, 3) for k, v in phases.items()},
-            "placement": placement,
-            "d2h_bytes_per_step": ((16 if ws > 1 else 12) * P) if placement == "host" else 0,
+            "placement": placement, "write_back": write_back,
+            "d2h_bytes_per_step": d2h,
             "note": ("host outer model (reference semantics); D2H of delta, (avg,) θ, momentum"
                      if placement == "host" else
                      "outer model in HBM (params/.grad/momentum are packed views); no PCIe")}
+
+
+def dropin_overlap(spec, dev, ws, rank, cycles, inner_ms=50.0):
+    """The host outer model in a training cycle: outer step, then `inner_ms` of GPU work
+    standing in for the inner steps that follow (bf16 GEMMs; a T125 inner step of the
+    reference's batch 512 x 1024 tokens is several times longer), then a device synchronize
+    as src/train.py:243 does. Exposed outer-step cost = cycle - inner work alone, for the
+    sync write-back and the deferred one (whose PCIe DMAs run under the inner work)."""
+    n = 8192
+    a = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    c = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
+
+    def gemms(k):
+        for _ in range(k):
+            torch.mm(a, b, out=c)
+
+    gemms(3)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gemms(10)
+    torch.cuda.synchronize()
+    per = (time.perf_counter() - t0) / 10
+    k = max(1, int(round(inner_ms * 1e-3 / per)))
+    t0 = time.perf_counter()
+    for _ in range(cycles):
+        gemms(k)
+        torch.cuda.synchronize()
+    t_in = _max_over_ranks((time.perf_counter() - t0) / cycles, dev, ws)
+    out = {"tree": spec.name, "inner_work_ms": round(t_in * 1e3, 3),
+           "inner_work": f"{k} bf16 GEMMs {n}^3 per cycle"}
+    P = spec.total()
+    for wb in ("sync", "deferred"):
+        r = dropin_rate(spec, dev, ws, rank, cycles, "host", wb, lambda: gemms(k))
+        exposed = max(r["ms_per_step"] - t_in * 1e3, 1e-3)
+        out[wb] = {"cycle_ms": r["ms_per_step"], "exposed_outer_ms": round(exposed, 3),
+                   "value": round(ws * 4.0 * P / (exposed * 1e-3) / 1e9, 2),
+                   "phase_ms": r["phase_ms"], "d2h_bytes_per_step": r["d2h_bytes_per_step"]}
+    out["unit"] = "GB/s"
+    out["note"] = ("value = N·4P / exposed outer-step time (cycle - inner work alone), host "
+                   "outer model (reference placement), PCIe included")
+    return out
 
 
 def gradsync_rate(spec, dev, ws, rank, steps):
@@ -848,6 +901,12 @@ class _Emitter:
         self.line, self.running, self.skipped = None, "headline", []
         self.lock = threading.Lock()
         self.done = False
+        # the JSON line goes to the process's original stdout; everything else written to
+        # fd 1 during the run (gloo's C++ "[Gloo] Rank ..." notices, library chatter) has
+        # been sent to stderr, so stdout carries exactly one line
+        sys.stdout.flush()
+        self.out_fd = os.dup(1)
+        os.dup2(2, 1)
         self.timer = threading.Timer(deadline_s, self._fire)
         self.timer.daemon = True
         self.timer.start()
@@ -863,7 +922,9 @@ class _Emitter:
             if self.rank == 0 and self.line is not None:
                 if self.skipped:
                     self.line["skipped_legs"] = self.skipped
-                print(json.dumps(self.line), flush=True)
+                buf = (json.dumps(self.line) + "\n").encode()
+                while buf:
+                    buf = buf[os.write(self.out_fd, buf):]
 
     def _fire(self):
         log(f"watchdog: {self.deadline:.0f} s reached while running {self.running!r}")
@@ -1067,6 +1128,8 @@ def main():
             em.line["dropin_pcie"] = leg("dropin_pcie", dropin_rate, spec, dev, ws, rank, 5,
                                          into={}, brief=False)
             leg(f"{spec.name}_dropin_device", dropin_rate, spec, dev, ws, rank, 10, "device",
+                brief=False)
+            leg(f"{spec.name}_dropin_overlap", dropin_overlap, spec, dev, ws, rank, 5,
                 brief=False)
         if ws == 1 and not a.no_cpu_baseline:
             # rank 0 at N = 1 only (the reference's CPU path on this host's cores)

@@ -16,6 +16,16 @@ HIP segment-walker kernels. Coherence is tracked with PyTorch's per-tensor versi
 a host tensor modified in place by torch code (e.g. the reference's CPU SGD) has a new
 `_version`, and the device copy is re-uploaded before its next use. Writes through `.data`
 bypass version counters; call `invalidate()` after such writes.
+
+Write-back (`write_back=`): "sync" (default) ends every call with the host tensors holding
+the new values, as the reference does. "deferred" (pinned write-back) keeps
+the device copy authoritative through the outer step and writes every arena the step changed
+back to the host in ONE batch of DMAs, issued at the end of `copy_to_inner`
+(sync_inner_model, src/train.py:269) on a side stream and not waited for: the PCIe transfer
+overlaps the next inner steps instead of sitting on the outer step's critical path. Until it
+completes the host tensors are stale; the next mirror call (and `flush()`, the outer model's
+`state_dict()`, `OuterSGD.state_dict()`) waits for it. A host tensor modified while its
+device copy is newer is an error, not a silent overwrite.
 """
 from __future__ import annotations
 
@@ -41,9 +51,14 @@ def _check_host_params(params: Sequence[torch.Tensor]) -> None:
             raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
 
 
+WRITE_BACKS = ("sync", "deferred")
+
+
 class HostOuterMirror:
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
-                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS):
+                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, write_back: str = "sync"):
+        if write_back not in WRITE_BACKS:
+            raise ValueError(f"write_back {write_back!r}: one of {WRITE_BACKS}")
         self.params: List[torch.nn.Parameter] = list(outer_model.parameters())
         if not self.params:
             raise ValueError("outer model has no parameters")
@@ -64,6 +79,14 @@ class HostOuterMirror:
         self._theta_key = None
         self._grad_key = None
         self._mom_key = None
+        # deferred write-back: arenas whose device copy is newer than the host, and the event
+        # of the write-back DMAs in flight
+        self.deferred = write_back == "deferred"
+        self._dirty: set = set()
+        self._wb_event = None
+        self._mom_bufs: Optional[List[torch.Tensor]] = None
+        self._wb_stream = (torch.cuda.Stream(self.device)
+                           if self.deferred and self.device.type == "cuda" else None)
         self._relay_params()
 
     # ---- host arenas ---------------------------------------------------------------------
@@ -103,6 +126,7 @@ class HostOuterMirror:
             self._relay_params()
         key = self._param_key()
         if key != self._theta_key:
+            self._conflict("theta", "outer parameters")
             self.d_theta.copy_(self.h_theta, non_blocking=True)
             self._theta_key = key
 
@@ -116,6 +140,7 @@ class HostOuterMirror:
         """Make d_wire equal the host gradients (missing ones per the caller's rule)."""
         if self._grad_key is not None and self._grad_key == self._grad_key_now():
             return
+        self._conflict("grad", "outer gradients")
         with torch.no_grad():
             for i, p in enumerate(self.params):
                 v = self._view(self.h_grad, i)
@@ -132,14 +157,64 @@ class HostOuterMirror:
         self._grad_key = self._grad_key_now()
 
     def _grads_to_host(self) -> None:
-        self.h_grad.copy_(self.d_wire, non_blocking=True)
         self._set_grad_views()
-        self._stream_sync()
+        if self.deferred:
+            self._dirty.add("grad")
+        else:
+            self.h_grad.copy_(self.d_wire, non_blocking=True)
+            self._stream_sync()
         self._grad_key = self._grad_key_now()
+
+    # ---- deferred write-back ----------------------------------------------------------------
+    def _conflict(self, arena: str, what: str) -> None:
+        if arena in self._dirty:
+            raise RuntimeError(
+                f"the host {what} changed while the device copy was newer (write_back="
+                "'deferred' writes them back at sync_inner_model); call flush() before "
+                "modifying them between the outer step's calls")
+
+    def _settle(self) -> None:
+        """Wait for the write-back DMAs in flight (host tensors valid afterwards)."""
+        if self._wb_event is not None:
+            self._wb_event.synchronize()
+            self._wb_event = None
+
+    def _write_back(self) -> None:
+        """Every dirty arena device -> host, on the side stream after the current stream's
+        work; not waited for (the next call or flush() settles it)."""
+        if not self._dirty:
+            return
+        pairs = {"grad": (self.h_grad, self.d_wire), "theta": (self.h_theta, self.d_theta),
+                 "mom": (self.h_mom, self.d_mom)}
+        if self._wb_stream is None:  # a CPU mirror (tests): plain copies
+            for a in self._dirty:
+                pairs[a][0].copy_(pairs[a][1])
+        else:
+            self._wb_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._wb_stream):
+                for a in ("grad", "theta", "mom"):
+                    if a in self._dirty:
+                        pairs[a][0].copy_(pairs[a][1], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._wb_stream)
+            self._wb_event = ev
+        # an arena write bumps the version counter its views share (.grad, momentum buffers;
+        # not the parameters, whose .data was set): these writes are ours, not the user's
+        if "grad" in self._dirty:
+            self._grad_key = self._grad_key_now()
+        if "mom" in self._dirty and self._mom_bufs is not None:
+            self._mom_key = tuple((b.data_ptr(), b._version) for b in self._mom_bufs)
+        self._dirty.clear()
+
+    def flush(self) -> None:
+        """Host tensors equal the device state (deferred mode; a no-op otherwise)."""
+        self._write_back()
+        self._settle()
 
     # ---- the four reference operations --------------------------------------------------
     def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
         """outer.grad = outer - inner (src/utils.py:218-221), delta computed in HBM."""
+        self._settle()
         self.theta_to_device()
         self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
         self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
@@ -147,6 +222,7 @@ class HostOuterMirror:
 
     def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
         """grad = Σ_peers grad / n (src/comm.py:120-123): RCCL on d_wire, /n in HBM."""
+        self._settle()
         self.grads_to_device(zero_fill_missing=True)
 
         def view(b):
@@ -167,6 +243,7 @@ class HostOuterMirror:
         host_bufs: the optimizer's current momentum buffers (None = not created yet, i.e.
         the first step). Returns the momentum buffers to store in the optimizer state
         (views of the pinned h_mom arena)."""
+        self._settle()
         self.theta_to_device()
         self.grads_to_device(zero_fill_missing=False)
         first = True
@@ -183,6 +260,7 @@ class HostOuterMirror:
                 views = [self._view(self.h_mom, i) for i in range(len(self.params))]
                 key = tuple((b.data_ptr(), b._version) for b in host_bufs)
                 if key != self._mom_key:
+                    self._conflict("mom", "momentum buffers")
                     with torch.no_grad():
                         for b, v in zip(host_bufs, views):
                             if b.data_ptr() != v.data_ptr():
@@ -190,24 +268,36 @@ class HostOuterMirror:
                     self.d_mom.copy_(self.h_mom, non_blocking=True)
         self.k.unpack_sgd(self.tree, ALL, self.d_wire, 1, self.d_theta,
                           self.d_mom if momentum != 0 else None, lr, momentum, nesterov, first, -1)
-        self.h_theta.copy_(self.d_theta, non_blocking=True)
         bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
         if momentum != 0:
-            self.h_mom.copy_(self.d_mom, non_blocking=True)
             bufs = [self._view(self.h_mom, i) for i in range(len(self.params))]
-        self._stream_sync()
+        if self.deferred:
+            self._dirty.add("theta")
+            if momentum != 0:
+                self._dirty.add("mom")
+        else:
+            self.h_theta.copy_(self.d_theta, non_blocking=True)
+            if momentum != 0:
+                self.h_mom.copy_(self.d_mom, non_blocking=True)
+            self._stream_sync()
         self._theta_key = self._param_key()  # arena writes do not bump parameter versions
         if momentum != 0:
             self._mom_key = tuple((b.data_ptr(), b._version) for b in bufs)
+            self._mom_bufs = bufs
         return bufs
 
     def copy_to_inner(self, inner_params: Sequence[torch.Tensor]) -> None:
-        """inner = outer (src/utils.py:223-226), scattered from HBM."""
+        """inner = outer (src/utils.py:223-226), scattered from HBM; deferred mode: then the
+        step's write-back to the host, in flight when this returns."""
+        self._settle()
         self.theta_to_device()
         self.k.bind(self.tree, SLOT_INNER, [p.data for p in inner_params], self.device)
         self.k.scatter(self.tree, ALL, self.d_theta, SLOT_INNER)
+        if self.deferred:
+            self._write_back()
 
     def close(self) -> None:
+        self.flush()
         self.tree.close()
 
 
@@ -289,6 +379,9 @@ class DeviceOuterMirror:
                     p.grad = v
 
     def invalidate(self) -> None:  # the arenas are the tensors: nothing is cached
+        pass
+
+    def flush(self) -> None:  # nothing is written back: torch copies to the host on demand
         pass
 
     # ---- the four reference operations --------------------------------------------------

@@ -26,6 +26,13 @@ class OuterSGD(SGD):
 
         return outer_mirror(self._model)
 
+    def state_dict(self):
+        """torch.optim.SGD.state_dict, after a deferred write-back of the momentum landed."""
+        from .utils import flush_outer_model
+
+        flush_outer_model(self._model)
+        return super().state_dict()
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

@@ -18,6 +18,14 @@ DILOCO_OUTER_PLACEMENT environment variable, "host" if unset):
             .grad and momentum buffers are views of packed HBM arenas
             (mirror.DeviceOuterMirror); no PCIe traffic and no host synchronisation per outer
             step. Host copies are made lazily by torch (`.cpu()`, `state_dict()`).
+
+Write-back of the host placement (`get_outer_model(..., write_back=)`, default from
+DILOCO_HOST_WRITEBACK, "sync" if unset): "sync" -- every call returns with the host tensors
+updated, as the reference's do; "deferred" -- the device copy stays authoritative through the
+outer step and the step's results reach the host tensors in one batch of DMAs issued by
+sync_inner_model and not waited for, so the PCIe transfer overlaps the next inner steps
+(mirror.HostOuterMirror; `flush_outer_model`, the outer model's `state_dict()` and
+`OuterSGD.state_dict()` wait for it).
 """
 from __future__ import annotations
 
@@ -29,12 +37,13 @@ import torch.nn as nn
 from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
-from .mirror import DeviceOuterMirror, HostOuterMirror
+from .mirror import WRITE_BACKS, DeviceOuterMirror, HostOuterMirror
 from .optim import OuterSGD
 
 _ATTR = "_diloco_mirror"
 _OUTER = "_diloco_outer"
 _PLACEMENT = "_diloco_placement"
+_WRITE_BACK = "_diloco_write_back"
 PLACEMENTS = ("host", "device")
 
 
@@ -57,7 +66,8 @@ def outer_mirror(outer_model: nn.Module, device=None):
                 if not torch.cuda.is_available():
                     raise RuntimeError("the DiLoCo outer step runs on the GPU; no HIP device")
                 device = torch.device("cuda", torch.cuda.current_device())
-        m = HostOuterMirror(outer_model, torch.device(device), kernels=k)
+        m = HostOuterMirror(outer_model, torch.device(device), kernels=k,
+                            write_back=getattr(outer_model, _WRITE_BACK, "sync"))
         object.__setattr__(outer_model, _ATTR, m)  # not a submodule / not in state_dict
     return m
 
@@ -69,14 +79,20 @@ def _inner_device(inner_model: nn.Module) -> torch.device:
     return p.device
 
 
-def get_outer_model(inner_model: nn.Module, placement: str = None) -> nn.Module:
+def get_outer_model(inner_model: nn.Module, placement: str = None,
+                    write_back: str = None) -> nn.Module:
     """Initializes the outer model from the inner model (src/utils.py:213-216).
 
-    placement "host" (the reference's, default) or "device" (see the module docstring)."""
+    placement "host" (the reference's, default) or "device"; write_back "sync" (default) or
+    "deferred" for the host placement (see the module docstring)."""
     if placement is None:
         placement = os.environ.get("DILOCO_OUTER_PLACEMENT", "host")
     if placement not in PLACEMENTS:
         raise ValueError(f"placement {placement!r}: one of {PLACEMENTS}")
+    if write_back is None:
+        write_back = os.environ.get("DILOCO_HOST_WRITEBACK", "sync")
+    if write_back not in WRITE_BACKS:
+        raise ValueError(f"write_back {write_back!r}: one of {WRITE_BACKS}")
     outer_model = copy.deepcopy(inner_model)
     if placement == "host":
         outer_model = outer_model.to("cpu")
@@ -92,9 +108,22 @@ def get_outer_model(inner_model: nn.Module, placement: str = None) -> nn.Module:
         outer_model = outer_model.to(dev)
     object.__setattr__(outer_model, _OUTER, True)  # get_optimizer: SGD here is the outer SGD
     object.__setattr__(outer_model, _PLACEMENT, placement)
+    object.__setattr__(outer_model, _WRITE_BACK, write_back)
     if placement == "device":
         outer_mirror(outer_model)  # lay the parameters out in the packed HBM arena now
+    elif write_back == "deferred":
+        # a checkpoint of the outer model waits for the write-back in flight
+        outer_model.register_state_dict_pre_hook(lambda mod, prefix, keep_vars:
+                                                  flush_outer_model(mod))
     return outer_model
+
+
+def flush_outer_model(outer_model: nn.Module) -> None:
+    """Make the host tensors of an outer model (parameters, .grad, momentum buffers) current:
+    waits for a deferred write-back (a no-op for write_back="sync" and placement="device")."""
+    m = getattr(outer_model, _ATTR, None)
+    if m is not None:
+        m.flush()
 
 
 def compute_pseudo_gradient(inner_model: nn.Module, outer_model: nn.Module) -> None:

@@ -70,9 +70,13 @@ def _worker(rank, world, port, mode, num_stages, out):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
     rec = {}
-    if mode in ("dropin", "dropin_device"):
+    if mode in ("dropin", "dropin_device", "dropin_deferred"):
+        from diloco_amd.utils import flush_outer_model
+
+        deferred = mode == "dropin_deferred"
         inner = _micro_module(theta0, shapes)
-        outer = get_outer_model(inner, placement="device" if mode == "dropin_device" else None)
+        outer = get_outer_model(inner, placement="device" if mode == "dropin_device" else None,
+                                write_back="deferred" if deferred else None)
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
         assert type(opt).__name__ == "OuterSGD"
         from diloco_amd.utils import outer_mirror
@@ -85,15 +89,36 @@ def _worker(rank, world, port, mode, num_stages, out):
             with torch.no_grad():
                 for p, v in zip(inner.parameters(), vals):
                     p.copy_(torch.from_numpy(v).view(p.shape))
+            def host(ts):
+                return np.concatenate([t.detach().numpy().reshape(-1) for t in ts])
+
+            # deferred write-back: outer step 1 flushes after every call (the mid-sequence
+            # flush path), outer step 2 reads the host tensors only after sync_inner_model
+            mid = not deferred or s == 1
             compute_pseudo_gradient(inner, outer)
-            rec[f"delta_s{s}"] = np.concatenate([p.grad.numpy().reshape(-1) for p in outer.parameters()])
+            if deferred and s == 1:
+                flush_outer_model(outer)
+            if mid:
+                rec[f"delta_s{s}"] = host(p.grad for p in outer.parameters())
             comm.sync_gradients(outer)
-            rec[f"avg_s{s}"] = np.concatenate([p.grad.numpy().reshape(-1) for p in outer.parameters()])
+            if deferred and s == 1:
+                flush_outer_model(outer)
+            if mid:
+                rec[f"avg_s{s}"] = host(p.grad for p in outer.parameters())
+            elif len(world_.dp_ranks) > 1:  # still the previous step's averages on the host
+                assert host(p.grad for p in outer.parameters()).tobytes() == rec["avg_s1"].tobytes()
             opt.step()
-            rec[f"theta_s{s}"] = np.concatenate([p.detach().numpy().reshape(-1) for p in outer.parameters()])
-            rec[f"buf_s{s}"] = np.concatenate([opt.state[p]["momentum_buffer"].numpy().reshape(-1)
-                                               for p in outer.parameters()])
+            if deferred and s == 1:
+                flush_outer_model(outer)
+            if mid:
+                rec[f"theta_s{s}"] = host(outer.parameters())
+                rec[f"buf_s{s}"] = host(opt.state[p]["momentum_buffer"] for p in outer.parameters())
             sync_inner_model(outer, inner)
+            if not mid:
+                flush_outer_model(outer)
+                rec[f"avg_s{s}"] = host(p.grad for p in outer.parameters())
+                rec[f"theta_s{s}"] = host(outer.parameters())
+                rec[f"buf_s{s}"] = host(opt.state[p]["momentum_buffer"] for p in outer.parameters())
             rec[f"inner_s{s}"] = np.concatenate([p.detach().numpy().reshape(-1) for p in inner.parameters()])
     elif mode in ("engine", "engine_ar"):
         # engine: the default at n > 1, reduce-scatter -> shard SGD -> all-gather;
@@ -225,7 +250,8 @@ def _run(mode, world, num_stages=1):
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "engine", "engine_ar"])
+@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_deferred", "engine",
+                                  "engine_ar"])
 def test_two_peers_match_reference_bit_exact(mode):
     g = load_npz("micro_n2.npz")
     recs = _run(mode, 2)

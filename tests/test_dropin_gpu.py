@@ -49,20 +49,23 @@ def _flat(ts):
     return np.concatenate([t.detach().cpu().numpy().reshape(-1) for t in ts])
 
 
-def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=None):
+def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=None,
+                 write_back=None):
     """The reference's outer step sequence with the drop-in functions (this process = DP
     rank `rank` of `n`; the default process group must exist)."""
     from diloco_amd import synth
     from diloco_amd.comm import TrainingComm
     from diloco_amd.trees import get_tree
-    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
-                                  sync_inner_model)
+    from diloco_amd.utils import (compute_pseudo_gradient, flush_outer_model, get_optimizer,
+                                  get_outer_model, sync_inner_model)
     from diloco_amd.world import World
 
     spec = get_tree("micro")
     shapes = [s for _, s in spec.params()]
     inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cpu")
-    outer = get_outer_model(inner, placement)  # src/train.py:382: before the inner model moves
+    # src/train.py:382: before the inner model moves
+    outer = get_outer_model(inner, placement, write_back=write_back)
+    deferred = write_back == "deferred"
     inner = inner.to("cuda:0")
     if placement == "device":
         assert all(p.is_cuda for p in outer.parameters())
@@ -79,14 +82,31 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
         with torch.no_grad():
             for p, v in zip(inner.parameters(), vals):
                 p.copy_(torch.from_numpy(v).view(p.shape))
+        # deferred write-back: outer step 1 flushes after every call, step 2 reads the host
+        # tensors only after sync_inner_model's write-back (waited for by the flush)
+        mid = not deferred or s == 1
         compute_pseudo_gradient(inner, outer)
-        rec[f"delta_s{s}"] = _flat(p.grad for p in outer.parameters())
+        if deferred and mid:
+            flush_outer_model(outer)
+        if mid:
+            rec[f"delta_s{s}"] = _flat(p.grad for p in outer.parameters())
         comm.sync_gradients(outer)
-        rec[f"avg_s{s}"] = _flat(p.grad for p in outer.parameters())
+        if deferred and mid:
+            flush_outer_model(outer)
+        if mid:
+            rec[f"avg_s{s}"] = _flat(p.grad for p in outer.parameters())
         opt.step()
-        rec[f"theta_s{s}"] = _flat(outer.parameters())
-        rec[f"buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"] for p in outer.parameters())
+        if deferred and mid:
+            flush_outer_model(outer)
+        if mid:
+            rec[f"theta_s{s}"] = _flat(outer.parameters())
+            rec[f"buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"] for p in outer.parameters())
         sync_inner_model(outer, inner)
+        if not mid:
+            flush_outer_model(outer)
+            rec[f"delta_s{s}"] = rec[f"avg_s{s}"] = _flat(p.grad for p in outer.parameters())
+            rec[f"theta_s{s}"] = _flat(outer.parameters())
+            rec[f"buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"] for p in outer.parameters())
         torch.cuda.synchronize()
         rec[f"inner_s{s}"] = _flat(inner.parameters())
         if host_shift and s == 1:
@@ -103,15 +123,17 @@ def _init_single():
         dist.init_process_group("gloo", init_method=f"file://{f}", rank=0, world_size=1)
 
 
-@pytest.mark.parametrize("stock_sgd,placement", [(False, "host"), (True, "host"),
-                                                 (False, "device")])
-def test_dropin_single_peer_matches_reference(stock_sgd, placement):
+@pytest.mark.parametrize("stock_sgd,placement,write_back", [
+    (False, "host", "sync"), (True, "host", "sync"), (False, "device", "sync"),
+    (False, "host", "deferred")])
+def test_dropin_single_peer_matches_reference(stock_sgd, placement, write_back):
     """The reference's call sequence, outer model on the host (its placement) or in HBM
     (placement="device"); torch's own CPU SGD on the host outer model as
-    well (the mirror must see its in-place updates)."""
+    well (the mirror must see its in-place updates); the host placement with the deferred
+    write-back (side-stream DMAs issued by sync_inner_model)."""
     _init_single()
     g = load_npz("micro_n1.npz")
-    rec = _outer_steps(0, 1, stock_sgd=stock_sgd, placement=placement)
+    rec = _outer_steps(0, 1, stock_sgd=stock_sgd, placement=placement, write_back=write_back)
     for s in (1, 2):
         assert rec[f"delta_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()
         assert rec[f"avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()  # n=1: no sync
@@ -166,8 +188,9 @@ def _worker(rank, world, port, mode, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     rec = {}
-    if mode in ("dropin", "dropin_device"):
-        rec = _outer_steps(rank, world, placement="device" if mode == "dropin_device" else None)
+    if mode in ("dropin", "dropin_device", "dropin_deferred"):
+        rec = _outer_steps(rank, world, placement="device" if mode == "dropin_device" else None,
+                           write_back="deferred" if mode == "dropin_deferred" else None)
     elif mode in ("engine", "engine_ar"):
         from diloco_amd import synth
         from diloco_amd.outer import OuterSync
@@ -278,7 +301,8 @@ def _run(mode, world=2):  # noqa: D401
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "engine", "engine_ar"])
+@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_deferred", "engine",
+                                  "engine_ar"])
 def test_two_peers_on_gpu_match_reference(mode):
     g = load_npz("micro_n2.npz")
     for rec in _run(mode):

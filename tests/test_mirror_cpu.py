@@ -1,0 +1,135 @@
+"""The host outer model's deferred write-back (mirror.HostOuterMirror, write_back="deferred")
+on CPU, through the oracle kernel backend: the reference's call sequence of
+src/train.py:263-269 at one peer, host tensors stale until sync_inner_model and then equal to
+the reference's fixture, flush on checkpoint, and the error when the host is modified while
+the device copy is newer. The GPU side (side-stream DMAs) is tests/test_dropin_gpu.py."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_npz
+from diloco_amd import kernels, synth
+from diloco_amd.trees import get_tree
+from diloco_amd.utils import (compute_pseudo_gradient, flush_outer_model, get_optimizer,
+                              get_outer_model, sync_inner_model)
+from oracle_kernels import OracleKernels
+
+
+class _Cfg:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+SGD_CFG = _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True)
+
+
+@pytest.fixture(autouse=True)
+def _oracle_backend():
+    prev = kernels._DEFAULT
+    kernels.set_default_kernels(OracleKernels())
+    yield
+    kernels._DEFAULT = prev
+
+
+def _models(write_back):
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.from_numpy(v.copy()).view(s))
+                                       for v, s in zip(theta0, shapes)])
+    outer = get_outer_model(inner, write_back=write_back)
+    return inner, outer
+
+
+def _set_inner(inner, outer, step):
+    prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
+    with torch.no_grad():
+        for p, v in zip(inner.parameters(), synth.inner_tree(prev, step, 0)):
+            p.copy_(torch.from_numpy(v).view(p.shape))
+
+
+def _host(ts):
+    return np.concatenate([t.detach().numpy().reshape(-1) for t in ts])
+
+
+def test_deferred_write_back_lands_at_sync_inner_model():
+    g = load_npz("micro_n1.npz")
+    inner, outer = _models("deferred")
+    opt = get_optimizer(outer, SGD_CFG)
+    for s in (1, 2):
+        _set_inner(inner, outer, s)
+        before = _host(outer.parameters())
+        compute_pseudo_gradient(inner, outer)
+        opt.step()
+        # the device copy holds the step; the host tensors have not been written yet
+        assert _host(outer.parameters()).tobytes() == before.tobytes()
+        sync_inner_model(outer, inner)
+        assert _host(outer.parameters()).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert _host(p.grad for p in outer.parameters()).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        assert _host(opt.state[p]["momentum_buffer"]
+                     for p in outer.parameters()).tobytes() == g[f"buf_s{s}"].tobytes()
+        assert _host(inner.parameters()).tobytes() == g[f"theta_s{s}"].tobytes()
+
+
+def test_checkpoint_flushes_a_deferred_step():
+    g = load_npz("micro_n1.npz")
+    inner, outer = _models("deferred")
+    opt = get_optimizer(outer, SGD_CFG)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    opt.step()
+    sd = outer.state_dict()  # the pre-hook writes the step back first
+    assert _host(sd.values()).tobytes() == g["theta_s1"].tobytes()
+    osd = opt.state_dict()
+    assert _host(osd["state"][i]["momentum_buffer"]
+                 for i in range(len(osd["state"]))).tobytes() == g["buf_s1"].tobytes()
+
+
+@pytest.mark.parametrize("what", ["grad", "param", "momentum"])
+def test_host_write_while_device_is_newer_is_an_error(what):
+    inner, outer = _models("deferred")
+    opt = get_optimizer(outer, SGD_CFG)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    if what == "momentum":  # a first full step creates the buffers, the second one is dirty
+        opt.step()
+        sync_inner_model(outer, inner)
+        compute_pseudo_gradient(inner, outer)
+        opt.step()  # momentum and θ now newer on the device than on the host
+        bufs = [opt.state[p]["momentum_buffer"] for p in outer.parameters()]
+        with torch.no_grad():
+            bufs[0].add_(1.0)
+        compute_pseudo_gradient(inner, outer)
+        with pytest.raises(RuntimeError, match="write_back='deferred'"):
+            opt.step()
+        return
+    p0 = next(outer.parameters())
+    if what == "param":  # θ is newer on the device after the optimizer step
+        opt.step()
+        with torch.no_grad():
+            p0.add_(1.0)
+        with pytest.raises(RuntimeError, match="write_back='deferred'"):
+            sync_inner_model(outer, inner)
+        return
+    with torch.no_grad():
+        p0.grad.add_(1.0)
+    with pytest.raises(RuntimeError, match="write_back='deferred'"):
+        opt.step()
+    # after a flush the host state is authoritative again and the step runs
+    inner2, outer2 = _models("deferred")
+    opt2 = get_optimizer(outer2, SGD_CFG)
+    _set_inner(inner2, outer2, 1)
+    compute_pseudo_gradient(inner2, outer2)
+    flush_outer_model(outer2)
+    with torch.no_grad():
+        next(outer2.parameters()).grad.add_(0.0)
+    opt2.step()
+
+
+def test_sync_write_back_is_the_default_and_argument_errors():
+    inner, outer = _models(None)
+    compute_pseudo_gradient(inner, outer)
+    assert not outer._diloco_mirror.deferred
+    with pytest.raises(ValueError, match="write_back"):
+        get_outer_model(inner, write_back="lazy")
