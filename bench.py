@@ -73,6 +73,10 @@ def setup_dist(n_gpus):
     backend = os.environ.get("DILOCO_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local %= max(1, torch.cuda.device_count())
+        # the drop-in legs' DP group (TrainingComm.dp_group) too
+        os.environ.setdefault("DILOCO_DP_BACKEND", "gloo")
+        if "diloco_amd.comm" in sys.modules:
+            sys.modules["diloco_amd.comm"].DP_BACKEND = os.environ["DILOCO_DP_BACKEND"]
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if ws > 1:
