@@ -800,7 +800,8 @@ def _brief(r):
     return {k: r[k] for k in keep if k in r}
 
 
-def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too, dump=None):
+def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too, dump=None,
+                     extra_spec=None):
     """The legs that map peers' memory or run point-to-point traffic between GPUs: the direct
     exchange, its parity check, the link probe and the device p2p transport (even N). Run by
     the isolated child processes below; `dump(result)` is called after every leg so that a
@@ -819,6 +820,13 @@ def peer_access_legs(spec, dev, ws, rank, steps, warmup, cap, parity_too, dump=N
     dump(res)
     if ws % 2 == 0:  # header over gloo, framed payload over RCCL
         res["extra"]["p2p_device_transport"] = _guard(p2p_rate, spec, dev, ws, rank, 10)
+        dump(res)
+    if extra_spec is not None:  # the north star's 1.3B fp32 bucket set through the direct
+        # exchange (last: the largest peer mappings)
+        torch.cuda.empty_cache()
+        r = _guard(run_tree, extra_spec, dev, ws, rank, max(3, steps // 4), 1, torch.float32,
+                   cap, False, False, None, "xgmi_inner")
+        res["extra"][f"{extra_spec.name}_xgmi_inner_exchange"] = _brief(r) if "value" in r else r
         dump(res)
     return res
 
@@ -866,7 +874,8 @@ def isolated_legs(a, dev, ws, rank, timeout_s, which="peer", extra_env=None):
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port[0]), **(extra_env or {}))
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(ws), "--steps", str(a.steps),
-           "--warmup", str(a.warmup), "--tree", a.tree, "--bucket-mb", str(a.bucket_mb),
+           "--warmup", str(a.warmup), "--tree", a.tree, "--extra-tree", a.extra_tree,
+           "--bucket-mb", str(a.bucket_mb),
            "--deadline", str(max(30.0, timeout_s - 10)), "--child-legs", which,
            "--child-out", out] + (["--no-parity"] if a.no_parity else [])
     torch.cuda.synchronize()
@@ -887,6 +896,25 @@ def isolated_legs(a, dev, ws, rank, timeout_s, which="peer", extra_env=None):
         os.remove(out)
     _sync(ws)  # every parent is past its child before anyone moves on
     return res
+
+
+def _xgmi_efficiency(line, extra, tree, ws):
+    """The direct exchange on the 1.3B set against RCCL's all_reduce of the same bytes (the
+    parent's rccl_allreduce_ref_<tree> leg), as exchange_efficiency_<tree> does for the RCCL
+    step."""
+    r = extra.get(f"{tree}_xgmi_inner_exchange")
+    ref = extra.get(f"rccl_allreduce_ref_{tree}")
+    if not (isinstance(r, dict) and "ms_per_step" in r and isinstance(ref, dict)
+            and "all_reduce" in ref):
+        return
+    P = get_tree(tree).total()
+    bw = 2.0 * (ws - 1) / ws * 4 * P / (r["ms_per_step"] * 1e-3) / 1e9
+    arbw = ref["all_reduce"]["busbw_GBs"]
+    line[f"exchange_efficiency_{tree}_xgmi_inner"] = {
+        "step_ms": round(r["ms_per_step"], 3), "step_busbw_GBs": round(bw, 1),
+        "rccl_allreduce_busbw_GBs": arbw, "frac_of_rccl_allreduce": round(bw / arbw, 4),
+        "frac_of_link_peak": round(bw / ((ws - 1) * XGMI_LINK_GBS), 4),
+        "note": "direct peer-access exchange (exchange='xgmi_inner'), whole outer step"}
 
 
 class _Emitter:
@@ -984,7 +1012,8 @@ def main():
 
         args = (get_tree(a.tree), dev, ws, rank, a.steps, a.warmup, (a.bucket_mb << 20) // 4)
         if a.child_legs == "peer":
-            peer_access_legs(*args, not a.no_parity, dump)
+            es = (get_tree(a.extra_tree) if a.extra_tree not in ("none", a.tree) else None)
+            peer_access_legs(*args, not a.no_parity, dump, es)
         else:
             rccl_env_legs(*args, dump)
         threading_timer.done = True
@@ -1152,6 +1181,7 @@ def main():
                 if "extra" in r:
                     extra.update(r["extra"])
                     parity.update(r["parity"])
+                    _xgmi_efficiency(em.line, extra, a.extra_tree, ws)
                 else:
                     extra["peer_access_legs"] = r
                 log(f"peer_access_legs done at {em.elapsed():.1f} s")
