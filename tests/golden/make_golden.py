@@ -8,7 +8,7 @@ PYTHONDONTWRITEBYTECODE=1 so nothing is written under /root/reference.
 Outputs (tests/golden/):
   trees.json         parameters() names/shapes of the micro/tiny/t125/t1.3b trees
                      (src/model.py GPT2 built on the meta device)
-  micro_n{1,2,4}.npz full fp32 bytes of the reference's outer step on the micro tree:
+  micro_n{1,2,4,8}.npz full fp32 bytes of the reference's outer step on the micro tree:
                      compute_pseudo_gradient (src/utils.py:218) -> TrainingComm.sync_gradients
                      over gloo (src/comm.py:117) -> SGD-Nesterov from get_optimizer
                      (src/utils.py:59, lr 0.7, m 0.9) -> sync_inner_model (src/utils.py:223),
@@ -222,6 +222,22 @@ def run_outer(tree: str, n: int, steps: int, full: bool, port: int):
         return recs, digs
 
 
+def capture_micro(n: int, port: int):
+    """micro_n<n>.npz: the reference's 2 outer steps with n DP peers (gloo), full bytes."""
+    recs, _ = run_outer("micro", n, 2, True, port)
+    out = {"theta0": recs[0]["theta0"], "inner_s1_r0": recs[0]["inner_s1"]}
+    for s in (1, 2):
+        out[f"delta_s{s}_r0"] = recs[0][f"delta_s{s}"]
+        out[f"delta_s{s}_rlast"] = recs[-1][f"delta_s{s}"]
+        out[f"avg_s{s}"] = recs[0][f"avg_s{s}"]
+        out[f"theta_s{s}"] = recs[0][f"theta_s{s}"]
+        out[f"buf_s{s}"] = recs[0][f"buf_s{s}"]
+        for r in range(1, n):  # every rank holds the same averaged state
+            assert np.array_equal(recs[r][f"avg_s{s}"], out[f"avg_s{s}"])
+            assert np.array_equal(recs[r][f"theta_s{s}"], out[f"theta_s{s}"])
+    np.savez_compressed(os.path.join(HERE, f"micro_n{n}.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--worker", action="store_true")
@@ -229,12 +245,20 @@ def main():
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--full", action="store_true")
+    ap.add_argument("--micro-n", type=int, nargs="*", default=None,
+                    help="only (re)capture micro_n<N>.npz for these peer counts")
     a = ap.parse_args()
     if a.worker:
         worker(a.tree, a.out, a.steps, a.full)
         return
     if not os.path.isdir(REF):
         raise SystemExit("the reference is not mounted; fixtures are committed under tests/golden")
+    if a.micro_n:
+        port = 29711
+        for n in a.micro_n:
+            capture_micro(n, port)
+            port += 11
+        return
     # the reference is imported only in child processes (stubs on PYTHONPATH, no bytecode)
     subprocess.run([sys.executable, "-c",
                     f"import sys; sys.path.insert(0, {HERE!r}); import make_golden as m; "
@@ -242,20 +266,9 @@ def main():
                    check=True, env=_ref_env(), cwd="/tmp")
     capture_plans(HERE)
     port = 29611
-    for n in (1, 2, 4):
-        recs, _ = run_outer("micro", n, 2, True, port)
+    for n in (1, 2, 4, 8):
+        capture_micro(n, port)
         port += 7
-        out = {"theta0": recs[0]["theta0"], "inner_s1_r0": recs[0]["inner_s1"]}
-        for s in (1, 2):
-            out[f"delta_s{s}_r0"] = recs[0][f"delta_s{s}"]
-            out[f"delta_s{s}_rlast"] = recs[-1][f"delta_s{s}"]
-            out[f"avg_s{s}"] = recs[0][f"avg_s{s}"]
-            out[f"theta_s{s}"] = recs[0][f"theta_s{s}"]
-            out[f"buf_s{s}"] = recs[0][f"buf_s{s}"]
-            for r in range(1, n):  # every rank holds the same averaged state
-                assert np.array_equal(recs[r][f"avg_s{s}"], out[f"avg_s{s}"])
-                assert np.array_equal(recs[r][f"theta_s{s}"], out[f"theta_s{s}"])
-        np.savez_compressed(os.path.join(HERE, f"micro_n{n}.npz"), **out)
     tiny = {}
     for n in (1, 2, 4):
         recs, digs = run_outer("tiny", n, 2, False, port)

@@ -267,13 +267,15 @@ def test_two_peers_match_reference_bit_exact(mode):
         assert recs[1]["delta_s1"].tobytes() == g["delta_s1_rlast"].tobytes()
 
 
-@pytest.mark.parametrize("mode", ["dropin", "engine", "engine_ar"])
-def test_four_peers_match_reference_normwise(mode):
+@pytest.mark.parametrize("mode,world", [("dropin", 4), ("engine", 4), ("engine_ar", 4),
+                                        ("dropin", 8), ("engine", 8)])
+def test_four_and_eight_peers_match_reference_normwise(mode, world):
+    """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""
     from diloco_amd.trees import get_tree
 
     numels = get_tree("micro").numels()
-    g = load_npz("micro_n4.npz")
-    recs = _run(mode, 4)
+    g = load_npz(f"micro_n{world}.npz")
+    recs = _run(mode, world)
     for rec in recs:
         for s in (1, 2):
             for k in ("theta", "buf"):

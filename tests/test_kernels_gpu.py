@@ -533,11 +533,11 @@ def test_sharded_engine_single_rank_layout():
     e.close()
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
 def test_sharded_step_emulated_matches_reference(n):
     """The sharded variant of n replicas on one GPU, collectives emulated (reduce-scatter = sum
     of the replicas' wire buckets, peer r keeps slice r; all-gather = concatenation of the θ
-    shards): θ, momentum and inner bit-exact vs the reference at n <= 2, normwise at n = 4."""
+    shards): θ, momentum and inner bit-exact vs the reference at n <= 2, normwise at n = 4, 8."""
     from conftest import normwise_ok
 
     spec = get_tree("micro")

@@ -73,10 +73,11 @@ def test_oracle_matches_reference_micro_bit_exact(n):
         assert v.tobytes() == g[k].tobytes(), k
 
 
-def test_oracle_matches_reference_micro_n4_normwise():
+@pytest.mark.parametrize("n", [4, 8])  # 8: the north star's DP = 8
+def test_oracle_matches_reference_micro_normwise(n):
     spec = get_tree("micro")
-    g = load_npz("micro_n4.npz")
-    got = _run_oracle(spec, 4)
+    g = load_npz(f"micro_n{n}.npz")
+    got = _run_oracle(spec, n)
     for k in ("delta_s1_r0", "delta_s1_rlast"):
         assert got[k].tobytes() == g[k].tobytes(), k  # step-1 per-rank deltas are exact
     # from step 2 on, θ carries the step-1 summation-order difference
