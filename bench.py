@@ -11,7 +11,13 @@ rank, device-resident (θ_outer, momentum and the wire buffer live in HBM):
            (BASELINE config #2: the delta+pack kernels, no RCCL)
     N > 1  dl_delta_pack -> RCCL reduce_scatter -> dl_shard_sgd (/n, SGD on this rank's 1/n)
            -> RCCL all_gather(θ) -> dl_scatter to inner, bucketed and pipelined
-Same tree per rank at every N (weak scaling): value = N * 4 * params / t_step, max over ranks.
+Same tree per rank at every N (weak scaling). value = 4 * params / t_step (SURVEY.md §8d:
+"GB/s params reduced" = the bytes of ONE parameter tree reduced per DP step; max time over
+ranks); the weak-scaling aggregate N * 4 * params / t_step is reported beside it as
+"value_aggregate". At N = 1 the step is also timed cold (the 256 MiB Infinity Cache scrubbed
+between steps, outside the timed events: in training H inner steps run in between) next to
+the back-to-back (warm) rate, and a flat copy kernel of the same access shape gives the
+same-run copy ceiling the roofline fractions are also read against.
 Rank 0 prints ONE JSON line: the headline with its roofline kernel (HIP events, PMC traffic
 from profiles/) and the CPU baseline (N = 1), then side legs (other trees and wires, the
 one-pass kernel, parity self-checks, drop-in rates, and at N > 1 the replicated variant,
@@ -121,8 +127,68 @@ def kernel_entry(bytes_per_launch, ms, traffic=None, bound="hbm", peak=HBM_PEAK_
             "bytes_per_launch": bytes_per_launch, "avg_ms": round(ms, 5)}
 
 
+SCRUB_MIB = 512  # >= 2 x the 256 MiB Infinity Cache moved per scrub (read 512 + write 512)
+
+
+class Scrubber:
+    """Evicts the step's bytes from the Infinity Cache (and every L2) between cold steps:
+    a default-policy dl_copy of SCRUB_MIB MiB (1 GiB of traffic), enqueued outside the timed
+    events. In training H inner steps (forward/backward over far more than 256 MiB) run
+    between two outer steps, so the cold figure is the one a DiLoCo run sees."""
+
+    def __init__(self, dev):
+        n = (SCRUB_MIB << 20) // 4
+        self.a = torch.ones(n, device=dev)
+        self.b = torch.empty(n, device=dev)
+        self.s = torch.cuda.current_stream(dev).cuda_stream
+
+    def __call__(self):
+        _lib.call("dl_copy", self.a.data_ptr(), self.b.data_ptr(), self.a.numel() * 4, 0, self.s)
+        self.a, self.b = self.b, self.a
+
+    def close(self):
+        del self.a, self.b
+
+
+def copy_ceiling(dev, mib=1024, reps=10):
+    """What a two-stream kernel of the walker's access shape (dl_copy) moves on this box in
+    this run: read + written bytes / time over `reps` back-to-back copies of `mib` MiB (far
+    beyond the Infinity Cache), default and non-temporal policy. The roofline fractions are
+    read against it beside the 8 TB/s spec peak (boxes differ by ~15 %)."""
+    n = (mib << 20) // 4
+    a = torch.ones(n, device=dev)
+    b = torch.empty(n, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    out = {"bytes_per_copy": 2 * 4 * n}
+    for name, flags in (("plain", 0), ("nt", _lib.TUNE_NT_LOADS)):
+        _lib.call("dl_copy", a.data_ptr(), b.data_ptr(), 4 * n, flags, st)  # warm the launch
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            src, dst = (a, b) if i % 2 == 0 else (b, a)
+            _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 4 * n, flags, st)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out[f"{name}_GBs"] = round(2 * 4 * n / (ms * 1e-3) / 1e9, 1)
+    out["GBs"] = max(out["plain_GBs"], out["nt_GBs"])
+    del a, b
+    torch.cuda.empty_cache()
+    return out
+
+
+def with_copy_ceiling(entry, ceiling_gbs):
+    """A kernel_entry with its achieved rate also read against the same-run copy ceiling."""
+    if entry is None or not ceiling_gbs:
+        return entry
+    e = dict(entry)
+    e["copy_ceiling"] = ceiling_gbs
+    e["frac_vs_copy"] = round(e["achieved"] / ceiling_gbs, 4)
+    return e
+
+
 def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loops=True,
-             shard=None, exchange="rccl", tile=None):
+             shard=None, exchange="rccl", tile=None, cold=False):
     """Timed region (K outer steps, nothing else on the stream), then an instrumented pass of
     K more steps with HIP events between the kernels on the stream they run on (events in the
     timed region would cost the step ~35 us each), then the same kernels back to back."""
@@ -160,7 +226,8 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
     pmc = load_pmc(spec.name) if wire == torch.float32 else {}
     res = {"tree": spec.name, "params": P, "tensors": len(spec.params()),
            "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
-           "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * P / (dt / steps) / 1e9,
+           "ms_per_step": dt / steps * 1e3, "value": 4.0 * P / (dt / steps) / 1e9,
+           "value_aggregate": ws * 4.0 * P / (dt / steps) / 1e9,
            "wire": "bf16" if wire == torch.bfloat16 else "f32",
            "tile_chunks": eng.tile_chunks if single and not fuse else None,
            "variant": ("one replica: dl_delta_sgd (one pass)" if single and fuse
@@ -182,6 +249,37 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         }
     else:
         res["step_ms_instrumented"] = round(first, 4)
+    if single and cold:
+        # cold: the same kernels with the Infinity Cache scrubbed before every step (outside
+        # the events), as after H inner steps in training
+        scr = Scrubber(dev)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        for e in ev:
+            scr()
+            e[0].record()
+            if fuse:
+                eng.step()
+                e[1].record()
+            else:
+                eng.pseudo_gradient()
+                e[1].record()
+                eng.apply()
+                eng.steps_done += 1
+            e[2].record()
+        torch.cuda.synchronize()
+        scr.close()
+        c_first = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+        c_second = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+        c_step = sum(e[0].elapsed_time(e[2]) for e in ev) / steps
+        res["cold"] = {"step_ms": round(c_step, 5), "value": 4.0 * P / (c_step * 1e-3) / 1e9,
+                       "note": "Infinity Cache scrubbed before each step (512 MiB copy, "
+                               "outside the events); step = the kernels' event span"}
+        if fuse:
+            res["cold"]["kernels"] = {"delta_sgd": kernel_entry(24 * P, c_first)}
+        else:
+            res["cold"]["kernels"] = {
+                "delta_pack": kernel_entry((8 + wb) * P, c_first),
+                "unpack_sgd": kernel_entry((wb + 20) * P, c_second)}
     # the same kernels back to back (cold inputs: no Infinity-Cache reuse across kernels)
     reps = max(steps, 10)
 
@@ -299,7 +397,10 @@ def run_two_stages(spec, dev, ws, rank, steps, warmup, cap):
     _sync(ws)
     dt = _max_over_ranks(time.perf_counter() - t0, dev, ws)
     res = {"tree": spec.name, "stages": 2, "dp_per_stage": ws // 2,
-           "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * spec.total() / (dt / steps) / 1e9,
+           "ms_per_step": dt / steps * 1e3,
+           # two trees (one per stage group) reduced per step
+           "value": 2 * 4.0 * spec.total() / (dt / steps) / 1e9,
+           "value_aggregate": ws * 4.0 * spec.total() / (dt / steps) / 1e9,
            "variant": "reduce_scatter -> shard SGD -> all_gather" if eng.sharded
            else "all_reduce -> replicated SGD"}
     eng.close()
@@ -481,7 +582,8 @@ def run_q8(spec, dev, ws, rank, steps, warmup, cap):
     nb = eng.tree.n_buckets
     slot_bytes = eng.tree.n_chunks * Q8_SLOT
     res = {"tree": spec.name, "params": P, "buckets": nb, "chunks": eng.tree.n_chunks,
-           "ms_per_step": dt / steps * 1e3, "value": ws * 4.0 * P / (dt / steps) / 1e9,
+           "ms_per_step": dt / steps * 1e3, "value": 4.0 * P / (dt / steps) / 1e9,
+           "value_aggregate": ws * 4.0 * P / (dt / steps) / 1e9,
            "wire": "int8", "wire_bytes_per_param": round(slot_bytes / P, 4),
            "bus_bytes_per_step": 2.0 * (ws - 1) / ws * slot_bytes}
     if ws == 1:  # the three kernels, each over the whole tree, timed in place
@@ -638,7 +740,8 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync",
         d2h = (16 if ws > 1 and write_back == "sync" else 12) * P
     if inner_fn is not None:
         phases["inner_work_and_sync"] = phases.pop("sync_inner_model")
-    return {"tree": spec.name, "value": round(ws * 4.0 * P / dt / 1e9, 2), "unit": "GB/s",
+    return {"tree": spec.name, "value": round(4.0 * P / dt / 1e9, 2), "unit": "GB/s",
+            "value_aggregate": round(ws * 4.0 * P / dt / 1e9, 2),
             "ms_per_step": round(dt * 1e3, 3),
             "phase_ms": {k: round(v / steps * 1e3, 3) for k, v in phases.items()},
             "placement": placement, "write_back": write_back,
@@ -682,10 +785,10 @@ def dropin_overlap(spec, dev, ws, rank, cycles, inner_ms=50.0):
         r = dropin_rate(spec, dev, ws, rank, cycles, "host", wb, lambda: gemms(k))
         exposed = max(r["ms_per_step"] - t_in * 1e3, 1e-3)
         out[wb] = {"cycle_ms": r["ms_per_step"], "exposed_outer_ms": round(exposed, 3),
-                   "value": round(ws * 4.0 * P / (exposed * 1e-3) / 1e9, 2),
+                   "value": round(4.0 * P / (exposed * 1e-3) / 1e9, 2),
                    "phase_ms": r["phase_ms"], "d2h_bytes_per_step": r["d2h_bytes_per_step"]}
     out["unit"] = "GB/s"
-    out["note"] = ("value = N·4P / exposed outer-step time (cycle - inner work alone), host "
+    out["note"] = ("value = 4P / exposed outer-step time (cycle - inner work alone), host "
                    "outer model (reference placement), PCIe included")
     return out
 
@@ -711,7 +814,8 @@ def gradsync_rate(spec, dev, ws, rank, steps):
     dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
     P = spec.total()
     gs.close()
-    return {"tree": spec.name, "value": round(ws * 4.0 * P / dt / 1e9, 2), "unit": "GB/s",
+    return {"tree": spec.name, "value": round(4.0 * P / dt / 1e9, 2), "unit": "GB/s",
+            "value_aggregate": round(ws * 4.0 * P / dt / 1e9, 2),
             "ms_per_step": round(dt * 1e3, 4), "buckets": gs.tree.n_buckets}
 
 
@@ -767,13 +871,6 @@ def cpu_baseline(spec, seconds_budget=12.0):
     from oracle.torch_restatement import time_steps
 
     t, n = time_steps(spec.numels(), steps=2, threads=1, budget_s=seconds_budget)
-    model = ""
-    try:
-        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
-        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
-                      if l.startswith("Model name")), "")
-    except Exception:
-        pass
     return {
         "value": round(4.0 * spec.total() / t / 1e9, 4), "unit": "GB/s", "cores": 1,
         "kind": "port",
@@ -781,9 +878,64 @@ def cpu_baseline(spec, seconds_budget=12.0):
                    f"warm step, per-tensor torch CPU restatement of src/utils.py:218-226 + "
                    f"torch SGD-Nesterov (sync_gradients is a no-op at n=1), 1 thread; "
                    f"{t:.3f} s/step"),
-        "host": {"cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
-                 "model": model, "torch": torch.__version__},
+        "host": _host_info(),
     }
+
+
+def cpu_baseline_dist(spec, ws, rank, seconds_budget=12.0):
+    """§8d CPU baseline at N > 1: this process is one of N fresh CPU processes (GPUs hidden)
+    in a gloo group, each running the reference's per-tensor sequence on the full tree with
+    one thread -- delta, per-tensor gloo all_reduce(SUM) + /= n, torch SGD-Nesterov, copy-back
+    (oracle/torch_restatement.TorchOuterStep) -- N cores in all. Steps are counted so that the
+    timed sample lasts about `seconds_budget`; value = 4P / t_step (the metric's definition),
+    max time over ranks."""
+    sys.path.insert(0, HERE)
+    from oracle.torch_restatement import TorchOuterStep
+
+    torch.set_num_threads(1)
+    g = torch.Generator().manual_seed(rank)
+    inner = [torch.empty(n).uniform_(-0.03, 0.03, generator=g) for n in spec.numels()]
+    st = TorchOuterStep(inner, group=dist.group.WORLD)
+    for t in inner:
+        t.add_(torch.empty_like(t).uniform_(-1e-3, 1e-3, generator=g))
+    st.step()  # creates the momentum buffers (not timed)
+    dist.barrier()
+    t0 = time.perf_counter()
+    st.step()
+    one = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(one, op=dist.ReduceOp.MAX)
+    k = max(2, int(seconds_budget / max(float(one.item()), 1e-3)))
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        st.step()
+    dt = torch.tensor([(time.perf_counter() - t0) / k], dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    t = float(dt.item())
+    return {"value": round(4.0 * spec.total() / t / 1e9, 4), "unit": "GB/s", "cores": ws,
+            "kind": "port",
+            "sample": (f"{spec.name} full tree ({spec.total()} params) per process, {ws} CPU "
+                       f"processes (gloo, 1 thread each), {k} timed outer steps after 2: "
+                       f"per-tensor torch restatement of src/utils.py:218-226 + per-tensor "
+                       f"all_reduce/n (src/comm.py:120-123) + torch SGD-Nesterov; "
+                       f"{t:.3f} s/step"),
+            "host": _host_info()}
+
+
+def _host_info():
+    model = ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
+                      if l.startswith("Model name")), "")
+    except Exception:
+        pass
+    return {"cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "model": model, "torch": torch.__version__}
+
+
+# CPU-baseline children see no GPU: they are host processes like the reference's --device cpu
+HIDE_GPUS = {"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""}
 
 
 def _guard(fn, *a, **k):
@@ -795,8 +947,9 @@ def _guard(fn, *a, **k):
 
 
 def _brief(r):
-    keep = ("value", "ms_per_step", "roofline", "kernels", "buckets", "params", "wire", "variant",
-            "wire_bytes_per_param", "bus_bytes_per_step", "tile_chunks")
+    keep = ("value", "value_aggregate", "ms_per_step", "roofline", "kernels", "buckets", "params",
+            "wire", "variant", "wire_bytes_per_param", "bus_bytes_per_step", "tile_chunks",
+            "cold")
     return {k: r[k] for k in keep if k in r}
 
 
@@ -998,6 +1151,20 @@ def main():
     ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
 
+    if a.child_legs == "cpu_baseline":  # one CPU process of the N > 1 CPU baseline
+        ws, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+        timer = _Emitter(rank, a.deadline)
+        dist.init_process_group("gloo", timeout=timedelta(minutes=3))
+        r = cpu_baseline_dist(get_tree(a.tree), ws, rank)
+        if rank == 0:
+            with open(a.child_out + ".tmp", "w") as f:
+                json.dump(r, f)
+            os.replace(a.child_out + ".tmp", a.child_out)
+        timer.done = True
+        dist.barrier()
+        dist.destroy_process_group()
+        timer.timer.cancel()
+        return
     if a.child_legs:  # one isolated child of isolated_legs
         ws, rank, dev = setup_dist(a.gpus)
         threading_timer = _Emitter(rank, a.deadline)  # bounds the child too
@@ -1037,7 +1204,7 @@ def main():
     fallback = None
     try:
         main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap,
-                            b2b_loops=not a.no_b2b, tile=0)
+                            b2b_loops=not a.no_b2b, tile=0, cold=not a.only_headline)
     except Exception as e:  # N > 1: the replicated all-reduce step still gives the driver a line
         if ws == 1:
             raise
@@ -1046,9 +1213,27 @@ def main():
         main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap, False,
                             not a.no_b2b, False)
     extra, parity = {}, {}
+    ceiling = None
+    if not a.only_headline:
+        ceiling = _guard(copy_ceiling, dev)
+        log(f"copy ceiling {ceiling}")
+    cgbs = ceiling.get("GBs") if isinstance(ceiling, dict) else None
+    roof = main_res["roofline"]
+    if ws == 1:
+        roof = with_copy_ceiling(roof, cgbs)
+    cold = main_res.get("cold")
+    roof_cold = None
+    if cold:
+        ks = cold["kernels"]
+        dom = max(ks, key=lambda k: ks[k]["avg_ms"])
+        roof_cold = dict(with_copy_ceiling(ks[dom], cgbs), kernel=dom)
+        cold = dict(cold, value=round(cold["value"], 3),
+                    kernels={k: with_copy_ceiling(v, cgbs) for k, v in ks.items()})
     em.line = {
         "metric": METRIC,
         "value": round(main_res["value"], 3),
+        "value_aggregate": round(main_res["value_aggregate"], 3),
+        "value_cold": cold["value"] if cold else None,
         "unit": "GB/s",
         "n_gpus": ws,
         "steps": a.steps,
@@ -1068,9 +1253,12 @@ def main():
             "wire": a.wire, "buckets": main_res["buckets"], "chunks": main_res["chunks"],
             "parallelism": f"dp{ws}",
         },
-        "roofline": main_res["roofline"],
+        "roofline": roof,
+        "roofline_cold": roof_cold,
+        "copy_ceiling": ceiling,
         "cpu_baseline": None,
         "kernels": main_res.get("kernels"),
+        "cold": cold,
         "kernels_b2b": main_res.get("kernels_b2b"),
         "parity": None if a.no_parity or a.only_headline else parity,
         "dropin_pcie": None,
@@ -1103,7 +1291,7 @@ def main():
     if not a.only_headline:
         if ws == 1:
             leg(f"{spec.name}_fused_single", run_tree, spec, dev, ws, rank, a.steps, a.warmup,
-                wire, cap, True)
+                wire, cap, True, True, None, "rccl", None, True)
         if a.extra_tree != "none" and a.extra_tree != a.tree:
             es = get_tree(a.extra_tree)
             ks = max(3, a.steps // 4)
@@ -1165,10 +1353,22 @@ def main():
             leg(f"{spec.name}_dropin_overlap", dropin_overlap, spec, dev, ws, rank, 5,
                 brief=False)
         if ws == 1 and not a.no_cpu_baseline:
-            # rank 0 at N = 1 only (the reference's CPU path on this host's cores)
+            # rank 0 at N = 1 (the reference's CPU path on one of this host's cores)
             em.running = "cpu_baseline"
             log("timing the CPU baseline")
             em.line["cpu_baseline"] = cpu_baseline(spec)
+        elif ws > 1 and not a.no_cpu_baseline:
+            # N CPU processes under gloo (one per rank, GPUs hidden): the reference's sequence
+            # with its per-tensor all_reduce, N cores
+            left = a.deadline - _max_over_ranks(em.elapsed(), dev, ws) - 15
+            if left < 60:
+                em.skipped.append("cpu_baseline")
+            else:
+                em.running = "cpu_baseline (child processes)"
+                log("timing the CPU baseline (N CPU processes)")
+                em.line["cpu_baseline"] = isolated_legs(a, dev, ws, rank, min(150.0, left),
+                                                        "cpu_baseline", HIDE_GPUS)
+                log(f"cpu_baseline done at {em.elapsed():.1f} s")
         if ws > 1 and not a.no_xgmi:
             # last, in child processes: the direct peer-access exchange (IPC-mapped wires / θ,
             # one fused kernel), its parity check and the link probe

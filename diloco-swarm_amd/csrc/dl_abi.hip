@@ -71,6 +71,11 @@ namespace dl {
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 }  // namespace dl
 
+// Pointer-table uploads go through a small ring of pinned staging slots, each guarded by the
+// event of the copy that last read it, so dl_tree_bind never synchronises the host with the
+// stream (a DP sync rebinding reallocated .grad tensors every inner step stays asynchronous).
+constexpr int kStageRing = 4;
+
 struct dl_tree_s {
   int device = 0;
   int32_t nseg = 0;
@@ -78,10 +83,15 @@ struct dl_tree_s {
   std::vector<int64_t> numel, seg_off, bounds;
   std::vector<int32_t> bkt_chunk;  // first chunk of each bucket, + sentinel
   std::vector<dl::Chunk> chunks;
-  std::vector<int64_t> chunk_loff;  // host only: offset of each chunk inside its tensor
+  std::vector<int64_t> chunk_loff;  // offset of each chunk inside its tensor (host copy)
   dl::Chunk* d_chunks = nullptr;
+  int64_t* d_loff = nullptr;    // chunk_loff on the device (the resolve kernel's input)
   void** d_caddr = nullptr;     // [DL_MAX_SLOTS][nchunk] resolved chunk addresses
-  uint64_t* h_stage = nullptr;  // pinned staging for address-table uploads (nchunk entries)
+  uint64_t* d_segptr = nullptr; // [DL_MAX_SLOTS][nseg] tensor base addresses
+  uint64_t* h_stage = nullptr;  // pinned staging ring: kStageRing x nseg addresses
+  hipEvent_t stage_ev[kStageRing] = {};
+  bool stage_used[kStageRing] = {};
+  int stage_next = 0;
   std::vector<uint8_t> bound;   // slot bound?
   std::vector<uint8_t> slot_aligned;
   int32_t grid = 0;                 // 0 = one workgroup per chunk
@@ -164,17 +174,25 @@ DL_API int dl_tree_create_ex(const int64_t* numel, int32_t n, int64_t cap_elems,
 
   hipError_t e = hipGetDevice(&t->device);
   const size_t nch = t->chunks.empty() ? 1 : t->chunks.size();
+  const size_t nsg = n > 0 ? size_t(n) : 1;
   const size_t cbytes = nch * sizeof(dl::Chunk);
   const size_t abytes = size_t(DL_MAX_SLOTS) * nch * sizeof(void*);
   if (e == hipSuccess) e = hipMalloc(&t->d_chunks, cbytes);
+  if (e == hipSuccess) e = hipMalloc(&t->d_loff, nch * sizeof(int64_t));
   if (e == hipSuccess) e = hipMalloc(&t->d_caddr, abytes);
   if (e == hipSuccess) e = hipMemset(t->d_caddr, 0, abytes);
+  if (e == hipSuccess) e = hipMalloc(&t->d_segptr, size_t(DL_MAX_SLOTS) * nsg * sizeof(uint64_t));
   if (e == hipSuccess && !t->chunks.empty())
     e = hipMemcpy(t->d_chunks, t->chunks.data(), t->chunks.size() * sizeof(dl::Chunk),
                   hipMemcpyHostToDevice);
+  if (e == hipSuccess && !t->chunks.empty())
+    e = hipMemcpy(t->d_loff, t->chunk_loff.data(), t->chunks.size() * sizeof(int64_t),
+                  hipMemcpyHostToDevice);
   if (e == hipSuccess)
-    e = hipHostMalloc(reinterpret_cast<void**>(&t->h_stage), nch * sizeof(uint64_t),
+    e = hipHostMalloc(reinterpret_cast<void**>(&t->h_stage), kStageRing * nsg * sizeof(uint64_t),
                       hipHostMallocDefault);
+  for (int i = 0; i < kStageRing && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&t->stage_ev[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     int rc2 = hip_fail(e, "dl_tree_create");
     dl_tree_destroy(t);
@@ -186,8 +204,16 @@ DL_API int dl_tree_create_ex(const int64_t* numel, int32_t n, int64_t cap_elems,
 
 DL_API int dl_tree_destroy(dl_tree_t t) {
   if (!t) return DL_OK;
+  // uploads still in flight read the staging ring: let them land before freeing it
+  for (int i = 0; i < kStageRing; ++i)
+    if (t->stage_ev[i]) {
+      if (t->stage_used[i]) (void)hipEventSynchronize(t->stage_ev[i]);
+      (void)hipEventDestroy(t->stage_ev[i]);
+    }
   if (t->d_chunks) (void)hipFree(t->d_chunks);
+  if (t->d_loff) (void)hipFree(t->d_loff);
   if (t->d_caddr) (void)hipFree(t->d_caddr);
+  if (t->d_segptr) (void)hipFree(t->d_segptr);
   if (t->h_stage) (void)hipHostFree(t->h_stage);
   delete t;
   return DL_OK;
@@ -264,15 +290,24 @@ DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t
     return DL_OK;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // The previous table of this slot may still be read by queued kernels on `s`: the copy is
-  // stream-ordered behind them; the staging buffer is reused only after it has landed.
-  DL_HIP(hipStreamSynchronize(s), "dl_tree_bind(sync before stage)");
-  for (size_t c = 0; c < nch; ++c)
-    t->h_stage[c] = ptrs[t->chunks[c].seg] + uint64_t(t->chunk_loff[c]) * sizeof(float);
-  DL_HIP(hipMemcpyAsync(t->d_caddr + size_t(slot) * nch, t->h_stage, nch * sizeof(void*),
-                        hipMemcpyHostToDevice, s),
+  // Stream-ordered and host-asynchronous: the n tensor addresses go into the next staging
+  // slot of the ring (waiting only if that slot's previous upload -- kStageRing binds ago --
+  // has not landed), one n-entry copy to the device, then dl_resolve_chunks expands them into
+  // the slot's per-chunk address table. Kernels queued earlier on `s` still read the previous
+  // table; the rewrite is ordered behind them.
+  const int k = t->stage_next;
+  t->stage_next = (k + 1) % kStageRing;
+  if (t->stage_used[k]) DL_HIP(hipEventSynchronize(t->stage_ev[k]), "dl_tree_bind(stage slot)");
+  uint64_t* stage = t->h_stage + size_t(k) * size_t(n);
+  for (int32_t i = 0; i < n; ++i) stage[i] = ptrs[i];
+  uint64_t* segptr = t->d_segptr + size_t(slot) * size_t(n);
+  DL_HIP(hipMemcpyAsync(segptr, stage, size_t(n) * sizeof(uint64_t), hipMemcpyHostToDevice, s),
          "dl_tree_bind(upload)");
-  DL_HIP(hipStreamSynchronize(s), "dl_tree_bind(sync after upload)");
+  DL_HIP(hipEventRecord(t->stage_ev[k], s), "dl_tree_bind(event)");
+  t->stage_used[k] = true;
+  DL_HIP(dl::launch_resolve_chunks(t->d_chunks, t->d_loff, segptr, int32_t(nch),
+                                   t->d_caddr + size_t(slot) * nch, s),
+         "dl_tree_bind(resolve)");
   t->bound[slot] = 1;
   return DL_OK;
 }
@@ -502,8 +537,32 @@ DL_API int dl_enable_peer_access(int32_t peer) {
 }
 
 DL_API int dl_sys_fence(dl_stream_t s) {
-  hipError_t e = dl::launch_sys_fence(static_cast<hipStream_t>(s));
+  hipError_t e = dl::launch_sys_fence(nullptr, nullptr, static_cast<hipStream_t>(s));
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_sys_fence");
+}
+
+DL_API int dl_sys_fence_census(uint32_t* xcc, int32_t cap, int32_t* grid, dl_stream_t s) {
+  if (!xcc || !grid) return fail(DL_E_ARG, "dl_sys_fence_census: null argument");
+  int dev = 0, n = 0;
+  DL_HIP(hipGetDevice(&dev), "dl_sys_fence_census");
+  DL_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev),
+         "dl_sys_fence_census");
+  if (cap < n)
+    return fail(DL_E_ARG, "dl_sys_fence_census: %d entries for %d workgroups", cap, n);
+  hipError_t e = dl::launch_sys_fence(xcc, grid, static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_sys_fence_census");
+}
+
+DL_API int dl_copy(const void* src, void* dst, int64_t bytes, int32_t flags, dl_stream_t s) {
+  if (bytes < 0 || bytes % 16) return fail(DL_E_ARG, "dl_copy: bytes %lld (multiple of 16)",
+                                           (long long)bytes);
+  if (bytes == 0) return DL_OK;
+  DL_TRY(check_packed(src, "dl_copy", "src"));
+  DL_TRY(check_packed(dst, "dl_copy", "dst"));
+  if (flags & ~DL_TUNE_NT_LOADS) return fail(DL_E_ARG, "dl_copy: flags 0x%x", flags);
+  hipError_t e = dl::launch_copy(src, dst, bytes / 16, (flags & DL_TUNE_NT_LOADS) != 0,
+                                 static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_copy");
 }
 
 DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each, void* dst,

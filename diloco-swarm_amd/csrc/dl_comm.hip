@@ -28,6 +28,10 @@ struct Rccl {
   decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   decltype(&ncclGetVersion) get_version = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
 };
 
 std::mutex g_mu;
@@ -54,7 +58,9 @@ int bind(void* h, const char* what) {
       !sym(h, "ncclReduceScatter", &r.reduce_scatter) ||
       !sym(h, "ncclAllGather", &r.all_gather) ||
       !sym(h, "ncclGetErrorString", &r.error_string) ||
-      !sym(h, "ncclGetVersion", &r.get_version))
+      !sym(h, "ncclGetVersion", &r.get_version) || !sym(h, "ncclSend", &r.send) ||
+      !sym(h, "ncclRecv", &r.recv) || !sym(h, "ncclGroupStart", &r.group_start) ||
+      !sym(h, "ncclGroupEnd", &r.group_end))
     return err(DL_E_STATE, "dl_rccl_load: %s lacks an RCCL entry point", what);
   g_rccl = r;
   return DL_OK;
@@ -189,6 +195,44 @@ DL_API int dl_all_gather(const void* send, void* recv, int64_t send_count, int32
   ncclResult_t r = g_rccl.all_gather(send, recv, size_t(send_count), nt,
                                      static_cast<ncclComm_t>(comm), static_cast<hipStream_t>(s));
   return r == ncclSuccess ? DL_OK : rccl_fail(r, "dl_all_gather");
+}
+
+/* Point-to-point (the payload leg of the device pipeline transport,
+ * replacing the reference's dist.send / dist.recv of a host copy, src/comm.py:38,67).
+ * Calls between dl_group_start and dl_group_end are issued as one RCCL group (a send and
+ * its matching receive on one rank -- a self send -- must be grouped). */
+DL_API int dl_send(const void* buf, int64_t count, int32_t dtype, int32_t peer, dl_comm_t comm,
+                   dl_stream_t s) {
+  ncclDataType_t nt;
+  size_t eb;
+  DL_RCCL_ARGS("dl_send", comm, dtype);
+  if (count < 0 || (count > 0 && !buf) || peer < 0) return err(DL_E_ARG, "dl_send: bad argument");
+  ncclResult_t r = g_rccl.send(buf, size_t(count), nt, peer, static_cast<ncclComm_t>(comm),
+                               static_cast<hipStream_t>(s));
+  return r == ncclSuccess ? DL_OK : rccl_fail(r, "dl_send");
+}
+
+DL_API int dl_recv(void* buf, int64_t count, int32_t dtype, int32_t peer, dl_comm_t comm,
+                   dl_stream_t s) {
+  ncclDataType_t nt;
+  size_t eb;
+  DL_RCCL_ARGS("dl_recv", comm, dtype);
+  if (count < 0 || (count > 0 && !buf) || peer < 0) return err(DL_E_ARG, "dl_recv: bad argument");
+  ncclResult_t r = g_rccl.recv(buf, size_t(count), nt, peer, static_cast<ncclComm_t>(comm),
+                               static_cast<hipStream_t>(s));
+  return r == ncclSuccess ? DL_OK : rccl_fail(r, "dl_recv");
+}
+
+DL_API int dl_group_start(void) {
+  if (int rc = ready("dl_group_start")) return rc;
+  ncclResult_t r = g_rccl.group_start();
+  return r == ncclSuccess ? DL_OK : rccl_fail(r, "dl_group_start");
+}
+
+DL_API int dl_group_end(void) {
+  if (int rc = ready("dl_group_end")) return rc;
+  ncclResult_t r = g_rccl.group_end();
+  return r == ncclSuccess ? DL_OK : rccl_fail(r, "dl_group_end");
 }
 
 }  // extern "C"

@@ -50,7 +50,9 @@ struct XgmiPeers {
 // delta: p.wire[] holds the peers' packed inner parameters (dl_xgmi_delta_sgd)
 hipError_t launch_xgmi_reduce_sgd(const XgmiPeers& p, int32_t n, int32_t rank, int64_t lo,
                                   int64_t len, float* mom, SgdArgs a, bool delta, hipStream_t s);
-hipError_t launch_sys_fence(hipStream_t s);
+// xcc (may be null): one entry per workgroup, the XCD (HW_REG_XCC_ID) it ran on; *grid_out
+// (may be null) = the grid size used (one 64-lane workgroup per CU of the current device)
+hipError_t launch_sys_fence(uint32_t* xcc, int32_t* grid_out, hipStream_t s);
 hipError_t launch_peer_gather(const XgmiPeers& p, int32_t nsrc, int32_t each4, float* dst,
                               hipStream_t s);
 
@@ -77,5 +79,10 @@ hipError_t launch_serialize(const void* src, int src_dtype, int64_t numel, float
                             float* out, hipStream_t s);
 hipError_t launch_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id,
                              float base, float scale, const float* add, hipStream_t s);
+// dl_tree_bind: out[c] = segptr[chunks[c].seg] + 4 * loff[c] for every chunk c
+hipError_t launch_resolve_chunks(const Chunk* chunks, const int64_t* loff, const uint64_t* segptr,
+                                 int32_t nch, void** out, hipStream_t s);
+// flat 16-B streaming copy (the same-run copy ceiling of bench.py): n16 float4, nt = NT policy
+hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, hipStream_t s);
 
 }  // namespace dl

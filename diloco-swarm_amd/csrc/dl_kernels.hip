@@ -345,9 +345,65 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+// dl_tree_bind's table expansion: the address of every chunk inside its bound tensor
+__global__ void __launch_bounds__(kThreads)
+    k_resolve_chunks(const Chunk* __restrict__ chunks, const int64_t* __restrict__ loff,
+                     const uint64_t* __restrict__ segptr, int32_t nch, uint64_t* __restrict__ out) {
+  for (int32_t c = int32_t(blockIdx.x) * kThreads + int32_t(threadIdx.x); c < nch;
+       c += int32_t(gridDim.x) * kThreads)
+    out[c] = segptr[chunks[c].seg] + uint64_t(loff[c]) * sizeof(float);
+}
+
+// Calibration copy: the walker's access shape (one workgroup per 16 KiB, every 16-B load of
+// the workgroup issued before its stores) on one flat buffer -- what the memory system gives
+// a two-stream kernel on this box in this run (bench.py's copy ceiling).
+template <bool NT>
+__global__ void __launch_bounds__(kThreads)
+    k_copy(const float* __restrict__ src, float* __restrict__ dst, int64_t n16) {
+  const int64_t base = int64_t(blockIdx.x) * (kThreads * kUnroll);
+  float4 x[kUnroll];
+  const float* s = src + base * 4;
+  float* d = dst + base * 4;
+  const int64_t rem = n16 - base;
+#pragma unroll
+  for (int u = 0; u < kUnroll; ++u) {
+    const int v = u * kThreads + int(threadIdx.x);
+    if (v < rem) x[u] = ldf4<NT>(s, v);
+  }
+#pragma unroll
+  for (int u = 0; u < kUnroll; ++u) {
+    const int v = u * kThreads + int(threadIdx.x);
+    if (v < rem) stf4<NT>(d, v, x[u]);
+  }
+}
+
 }  // namespace
 
 // ---- launchers -------------------------------------------------------------------------------
+hipError_t launch_resolve_chunks(const Chunk* chunks, const int64_t* loff, const uint64_t* segptr,
+                                 int32_t nch, void** out, hipStream_t s) {
+  if (nch <= 0) return hipSuccess;
+  int32_t grid = (nch + kThreads - 1) / kThreads;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(k_resolve_chunks, dim3(grid), dim3(kThreads), 0, s, chunks, loff, segptr,
+                     nch, reinterpret_cast<uint64_t*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, hipStream_t s) {
+  if (n16 <= 0) return hipSuccess;
+  const int64_t per = kThreads * kUnroll;
+  const int64_t grid = (n16 + per - 1) / per;
+  if (grid > INT32_MAX) return hipErrorInvalidValue;
+  if (nt)
+    hipLaunchKernelGGL(k_copy<true>, dim3(uint32_t(grid)), dim3(kThreads), 0, s,
+                       static_cast<const float*>(src), static_cast<float*>(dst), n16);
+  else
+    hipLaunchKernelGGL(k_copy<false>, dim3(uint32_t(grid)), dim3(kThreads), 0, s,
+                       static_cast<const float*>(src), static_cast<float*>(dst), n16);
+  return hipGetLastError();
+}
+
 hipError_t launch_delta_pack(const Launch& L, int inner_slot, const float* outer, void* wire,
                              int wire_dtype) {
   if (wire_dtype == DL_BF16)

@@ -119,19 +119,46 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
-// Cross-GPU ordering of coarse-grained buffers (dl_sys_fence): one workgroup per CU, each
-// issuing a system-scope fence (buffer_wbl2 sc0 sc1, then buffer_inv sc0 sc1) so that every
-// XCD's L2 has written back its dirty lines (peers reading this GPU's memory over xGMI see
-// them) and dropped its clean ones (stale copies of lines peers have since written here, or
-// of peers' memory). Workgroups are dispatched round-robin over the 8 XCDs.
-__global__ void __launch_bounds__(64) k_sys_fence() {
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+// Cross-GPU ordering of coarse-grained buffers (dl_sys_fence): one workgroup per CU (grid =
+// the device's multiProcessorCount), each issuing a system-scope fence (buffer_wbl2 sc0 sc1,
+// then buffer_inv sc0 sc1) so that every XCD's L2 has written back its dirty lines (peers
+// reading this GPU's memory over xGMI see them) and dropped its clean ones (stale copies of
+// lines peers have since written here, or of peers' memory). An XCD is covered if at least
+// one workgroup lands on it; with one workgroup per CU every XCD receives its share under
+// any placement that uses every CU. `xcc` (census, tests): each workgroup records the XCD it
+// ran on (s_getreg HW_REG_XCC_ID; a read, the record is a vector store), which
+// tests/test_fence_gpu.py checks covers all XCDs.
+__global__ void __launch_bounds__(64) k_sys_fence(uint32_t* __restrict__ xcc) {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+    if (xcc) {
+      uint32_t id;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
+      xcc[blockIdx.x] = id & 0xFu;
+    }
+  }
+}
+
+int32_t cu_count() {
+  static int32_t cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
 }
 
 }  // namespace
 
-hipError_t launch_sys_fence(hipStream_t s) {
-  hipLaunchKernelGGL(k_sys_fence, dim3(256), dim3(64), 0, s);
+hipError_t launch_sys_fence(uint32_t* xcc, int32_t* grid_out, hipStream_t s) {
+  const int32_t grid = cu_count();
+  if (grid_out) *grid_out = grid;
+  hipLaunchKernelGGL(k_sys_fence, dim3(grid), dim3(64), 0, s, xcc);
   return hipGetLastError();
 }
 

@@ -82,6 +82,12 @@ SIGNATURES = {
     "dl_can_access_peer": (ctypes.c_int, [_i32, _i32, _pi32]),
     "dl_enable_peer_access": (ctypes.c_int, [_i32]),
     "dl_sys_fence": (ctypes.c_int, [_vp]),
+    "dl_sys_fence_census": (ctypes.c_int, [_vp, _i32, _pi32, _vp]),
+    "dl_send": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
+    "dl_recv": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
+    "dl_group_start": (ctypes.c_int, []),
+    "dl_group_end": (ctypes.c_int, []),
+    "dl_copy": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp]),
     "dl_peer_gather": (ctypes.c_int, [_pu64, _i32, _i64, _vp, _vp]),
     "dl_xgmi_reduce_sgd": (
         ctypes.c_int,

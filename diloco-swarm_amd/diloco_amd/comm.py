@@ -34,8 +34,32 @@ from .gradsync import GradSync
 from .serializer import Metadata, Serializer
 
 
+class ThreadStopped(RuntimeError):
+    """A pipeline send/recv thread died; raised on the caller's side (the original exception
+    is the __cause__) instead of leaving the caller blocked on a queue forever."""
+
+
+STOPPED = object()  # queued by a dying receiver so that a blocked receive() wakes up
+
+
+def check_alive(thread) -> None:
+    if thread.error is not None:
+        raise ThreadStopped(f"{type(thread).__name__} stopped: {thread.error!r}") from thread.error
+
+
+def receive_or_raise(thread):
+    """queue.get() that raises ThreadStopped once the receiving thread has died."""
+    item = thread.queue.get()
+    if item is STOPPED:
+        thread.queue.put(STOPPED)  # every later receive() raises too
+        check_alive(thread)
+    return item
+
+
 class SendThread:
-    """Queue-fed sender (src/comm.py:16-38): optional framing, then dist.send from host memory."""
+    """Queue-fed sender (src/comm.py:16-38): optional framing, then dist.send from host memory.
+    An exception in the thread (e.g. framing a tensor the Serializer rejects) stops it and is
+    re-raised by the next send() call."""
 
     TIMEOUT = 1e-4
 
@@ -44,6 +68,7 @@ class SendThread:
         self.shape, self.group, self.tag, self.serialize = shape, group, tag, serialize
         self.logger = kwargs.get("logger")
         self.queue: Queue = Queue()
+        self.error: Optional[BaseException] = None
         if serialize:
             self.serializer = Serializer(shape)
             self.shape = self.serializer.shape
@@ -51,17 +76,22 @@ class SendThread:
             threading.Thread(target=self._send_loop, daemon=True).start()
 
     def send(self, dst: int, tensor: torch.Tensor, metadata: Optional[Metadata]) -> None:
+        check_alive(self)
         self.queue.put((dst, tensor, metadata))
 
     def _send_loop(self):
-        while True:
-            if self.queue.empty():
-                time.sleep(self.TIMEOUT)
-                continue
-            dst, tensor, metadata = self.queue.get()
-            if self.serialize:
-                tensor = self.serializer.serialize(tensor, metadata)
-            dist.send(tensor.to("cpu"), dst=dst, group=self.group, tag=self.tag)
+        try:
+            while True:
+                if self.queue.empty():
+                    time.sleep(self.TIMEOUT)
+                    continue
+                dst, tensor, metadata = self.queue.get()
+                if self.serialize:
+                    tensor = self.serializer.serialize(tensor, metadata)
+                dist.send(tensor.to("cpu"), dst=dst, group=self.group, tag=self.tag)
+        except BaseException as e:
+            self.error = e
+            raise
 
 
 class RecvThread:
@@ -74,6 +104,7 @@ class RecvThread:
         self.requires_grad, self.dtype, self.serialize = requires_grad, dtype, serialize
         self.logger = kwargs.get("logger")
         self.queue: Queue = Queue()
+        self.error: Optional[BaseException] = None
         if serialize:
             self.serializer = Serializer(shape)
             self.shape = self.serializer.shape
@@ -88,16 +119,21 @@ class RecvThread:
         self.queue.put((-1, tensor, metadata))
 
     def receive(self):
-        return self.queue.get()
+        return receive_or_raise(self)
 
     def _recv_loop(self):
-        while True:
-            buf = torch.empty(self.shape, dtype=self.dtype, requires_grad=self.requires_grad)
-            src = dist.recv(buf, group=self.group, tag=self.tag)
-            meta = None
-            if self.serialize:
-                buf, meta = self.serializer.deserialize(buf)
-            self.queue.put((src, buf, meta))
+        try:
+            while True:
+                buf = torch.empty(self.shape, dtype=self.dtype, requires_grad=self.requires_grad)
+                src = dist.recv(buf, group=self.group, tag=self.tag)
+                meta = None
+                if self.serialize:
+                    buf, meta = self.serializer.deserialize(buf)
+                self.queue.put((src, buf, meta))
+        except BaseException as e:
+            self.error = e
+            self.queue.put(STOPPED)  # can_receive turns true; receive() raises
+            raise
 
 
 # Collective backend of the DP group for device tensors: "nccl" = RCCL over xGMI (the
@@ -138,12 +174,24 @@ class DPSync:
         params = list(model.parameters())
         if not params:
             return
-        from .utils import _OUTER, outer_mirror
+        from .utils import device_path, has_mirror, outer_mirror
 
-        if params[0].device.type == "cpu" or getattr(model, _OUTER, False):
-            # an outer model (host or device placement): its packed mirror reduces in place
+        if has_mirror(model):
+            # an outer model whose steps run on the GPU (host placement after a device
+            # compute_pseudo_gradient, or placement="device"): its packed mirror reduces
             m = outer_mirror(model)
             m.all_reduce(self.dp_group(m.device), num_peers)
+            return
+        if not device_path(params[0]):
+            # host tensors (the reference's --device cpu runs, or an outer model not yet
+            # touched by a device step): the reference's loop on its gloo stage group
+            group = self.world.curr_stage_group
+            with torch.no_grad():
+                for p in params:
+                    if p.grad is None:
+                        p.grad = torch.zeros_like(p)
+                    dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=group)
+                    p.grad.div_(num_peers)
             return
         for p in params:
             if p.grad is None:

@@ -48,6 +48,13 @@ class OuterSGD(SGD):
                 "dampening=0, maximize=False")
         if g["nesterov"] and g["momentum"] == 0:
             raise ValueError("Nesterov momentum requires a momentum")
+        from .utils import device_path, has_mirror
+
+        if not has_mirror(self._model) and not device_path(g["params"][0]):
+            # host tensors never stepped on the GPU (the reference's --device cpu runs):
+            # torch.optim.SGD itself, as src/utils.py:62-63 builds it
+            super().step()
+            return loss
         mirror = self._mirror()
         params = g["params"]
         if len(params) != len(mirror.params) or any(a is not b for a, b in zip(params, mirror.params)):

@@ -64,6 +64,9 @@ class DeviceSendThread:
             threading.Thread(target=self._send_loop, daemon=True).start()
 
     def send(self, dst: int, tensor: torch.Tensor, metadata: Optional[Metadata]) -> None:
+        from .comm import check_alive
+
+        check_alive(self)
         self.queue.put((dst, tensor, metadata))
 
     def send_one(self, dst: int, tensor: torch.Tensor, metadata: Optional[Metadata]) -> None:
@@ -117,7 +120,9 @@ class DeviceRecvThread:
         self.queue.put((-1, tensor, metadata))
 
     def receive(self):
-        return self.queue.get()
+        from .comm import receive_or_raise
+
+        return receive_or_raise(self)
 
     def recv_one(self):
         hdr = torch.empty(1, dtype=torch.int64)
@@ -147,7 +152,10 @@ class DeviceRecvThread:
             try:
                 item = self.recv_one()
             except BaseException as e:
+                from .comm import STOPPED
+
                 self.error = e
+                self.queue.put(STOPPED)  # a blocked receive() wakes up and raises
                 raise
             self.queue.put(item)
 

@@ -52,6 +52,19 @@ def version() -> int:
     return v.value
 
 
+class group:
+    """RCCL group (dl_group_start / dl_group_end): the point-to-point calls inside progress
+    together -- required for a send and its receive on one rank."""
+
+    def __enter__(self):
+        _lib.call("dl_group_start")
+        return self
+
+    def __exit__(self, *exc):
+        _lib.call("dl_group_end")
+        return False
+
+
 class Comm:
     def __init__(self, handle: int, nranks: int, owned: bool):
         self.handle, self.nranks, self.owned = ctypes.c_void_p(handle), nranks, owned
@@ -103,6 +116,16 @@ class Comm:
             raise ValueError("all_gather: output must be nranks x input, same dtype")
         _lib.call("dl_all_gather", inp.data_ptr(), out.data_ptr(), inp.numel(), _dtype(inp),
                   self.handle, _stream(inp))
+
+    def send(self, t: torch.Tensor, peer: int) -> None:
+        """Point-to-point send of t to `peer` (src/comm.py:38 on the device, no host copy)."""
+        _lib.call("dl_send", t.data_ptr(), t.numel(), _dtype(t), int(peer), self.handle,
+                  _stream(t))
+
+    def recv(self, t: torch.Tensor, peer: int) -> None:
+        """Point-to-point receive into t from `peer` (src/comm.py:67 after the header)."""
+        _lib.call("dl_recv", t.data_ptr(), t.numel(), _dtype(t), int(peer), self.handle,
+                  _stream(t))
 
     def close(self) -> None:
         if self.owned and self.handle:

@@ -1,14 +1,19 @@
-"""Activation framing for SWARM point-to-point sends (src/serializer.py), on the GPU.
+"""Activation framing for SWARM point-to-point sends (src/serializer.py).
 
 Same interface and wire format as the reference: `Serializer(shape).shape == (2, *shape)`;
-`serialize(t, (a, b))` returns a (2, *t.shape) fp32 tensor whose plane 0 carries a, b as
-floats at flat indices 0 and 1 (the rest of plane 0 is unspecified: the reference leaves it
-uninitialised, src/serializer.py:12) and whose plane 1 is t promoted to fp32 (torch.cat's
-promotion of an fp32 metadata plane with an fp32/bf16/fp16 payload); `deserialize` returns
-(payload view, (int(a), int(b))).
+`serialize(t, (a, b))` returns a (2, *t.shape) tensor on t's device whose plane 0 carries a, b
+as floats at flat indices 0 and 1 (the rest of plane 0 is unspecified: the reference leaves
+it uninitialised, src/serializer.py:12) and whose plane 1 is t promoted with fp32 (torch.cat's
+promotion of the fp32 metadata plane with the payload: fp32/bf16/fp16 -> fp32, fp64 -> fp64);
+`deserialize` returns (payload view, (int(a), int(b))).
 
-serialize is one HIP kernel (dl_serialize: 2 metadata writes + a converting copy) instead of
-torch.empty + two indexed writes + reshape + cat. It frames device tensors only.
+Dispatch is on the payload's device, as the reference frames on `tensor.device`
+(src/serializer.py:12):
+  GPU  one HIP kernel (dl_serialize: 2 metadata writes + a converting copy) instead of
+       torch.empty + two indexed writes + reshape + cat; fp32/bf16/fp16 payloads. Without
+       libdiloco_hip.so this raises (no fallback for device tensors).
+  CPU  the same frame built with torch ops in host memory (the reference's --device cpu runs,
+       tests/test_memorize.py:35-39).
 """
 from __future__ import annotations
 
@@ -28,20 +33,30 @@ class Serializer:
         self.shape = (2, *shape)
 
     def serialize(self, tensor: torch.Tensor, metadata: Metadata) -> torch.Tensor:
-        if tensor.device.type != "cuda":
-            raise ValueError("diloco_amd.Serializer frames device tensors (HIP kernel); got "
-                             f"{tensor.device}")
-        if tensor.dtype not in _SRC:
-            raise TypeError(f"serialize: payload dtype {tensor.dtype} (fp32/bf16/fp16)")
         n = tensor.numel()
         if n < 2:  # the reference fails on metadata_tensor[1] for the same inputs
             raise IndexError(f"index {n} is out of bounds for dimension 0 with size {n}")
+        if tensor.device.type != "cuda":
+            return self._frame_host(tensor, metadata)
+        if tensor.dtype not in _SRC:
+            raise TypeError(f"serialize: payload dtype {tensor.dtype} (fp32/bf16/fp16)")
         src = tensor.detach().contiguous()
         out = torch.empty((2, *tensor.shape), dtype=torch.float32, device=tensor.device)
         _lib.call("dl_serialize", src.data_ptr(), _SRC[tensor.dtype], n, float(metadata[0]),
                   float(metadata[1]), out.data_ptr(),
                   torch.cuda.current_stream(tensor.device).cuda_stream)
         return out
+
+    @staticmethod
+    def _frame_host(tensor: torch.Tensor, metadata: Metadata) -> torch.Tensor:
+        """The frame in host memory: payload copied into plane 1 (with torch.cat's dtype
+        promotion and autograd), the two metadata floats written into plane 0."""
+        dtype = torch.promote_types(torch.float32, tensor.dtype)
+        meta = torch.empty(tensor.shape, dtype=torch.float32, device=tensor.device)
+        flat = meta.view(-1)  # the metadata values are fp32 first, as in the reference
+        flat[0] = float(metadata[0])
+        flat[1] = float(metadata[1])
+        return torch.stack([meta.to(dtype), tensor.to(dtype)])
 
     def deserialize(self, serialized: torch.Tensor) -> Tuple[torch.Tensor, Metadata]:
         meta = serialized[0].flatten()[:2].tolist()  # one device->host read for both values

@@ -1,6 +1,11 @@
 """Drop-in for the DiLoCo helpers of src/utils.py:203-226 and get_optimizer (src/utils.py:59-65).
 
-Same names, arguments and host-visible results as the reference; the work runs on the GPU:
+Same names, arguments and host-visible results as the reference. Dispatch is on the inner
+model's device, as the reference's `.to(param_outer.device)` / `.to(param_inner.device)`
+copies are (src/utils.py:221,226): a GPU inner model runs the HIP path below; a CPU inner
+model (the reference's --device cpu runs, tests/test_memorize.py:35-39) gets the reference's
+per-tensor torch ops on the host. The GPU path has no CPU fallback: without libdiloco_hip.so
+it raises. On the GPU:
 
   get_outer_model(inner)            deepcopy(inner).to("cpu")              src/utils.py:213-216
   compute_pseudo_gradient(in, out)  out.grad = out - in   (dl_delta_pack)   src/utils.py:218-221
@@ -45,6 +50,17 @@ _OUTER = "_diloco_outer"
 _PLACEMENT = "_diloco_placement"
 _WRITE_BACK = "_diloco_write_back"
 PLACEMENTS = ("host", "device")
+
+
+def device_path(t: torch.Tensor) -> bool:
+    """True when tensors on t's device take the HIP path: device tensors always; host tensors
+    only under a test backend that declares it computes on host tensors
+    (tests/oracle_kernels.py: accepts_host_tensors, installed with set_default_kernels)."""
+    return t.device.type != "cpu" or getattr(default_kernels(), "accepts_host_tensors", False)
+
+
+def has_mirror(outer_model: nn.Module) -> bool:
+    return getattr(outer_model, _ATTR, None) is not None
 
 
 def outer_mirror(outer_model: nn.Module, device=None):
@@ -126,8 +142,19 @@ def flush_outer_model(outer_model: nn.Module) -> None:
         m.flush()
 
 
+def _host_path(inner_model: nn.Module, outer_model: nn.Module) -> bool:
+    """The reference's host semantics apply: a CPU inner model and no device mirror."""
+    p = next(inner_model.parameters(), None)
+    return p is not None and not device_path(p) and not has_mirror(outer_model)
+
+
 def compute_pseudo_gradient(inner_model: nn.Module, outer_model: nn.Module) -> None:
     """outer.grad = outer - inner for every parameter (src/utils.py:218-221)."""
+    if _host_path(inner_model, outer_model):
+        with torch.no_grad():
+            for po, pi in zip(outer_model.parameters(), inner_model.parameters()):
+                po.grad = torch.sub(po.data, pi.data.to(po.device))  # a fresh tensor
+        return
     dev = _inner_device(inner_model)
     m = outer_mirror(outer_model, dev if dev.type != "cpu" else None)
     m.pseudo_gradient(list(inner_model.parameters()))
@@ -135,6 +162,11 @@ def compute_pseudo_gradient(inner_model: nn.Module, outer_model: nn.Module) -> N
 
 def sync_inner_model(outer_model: nn.Module, inner_model: nn.Module) -> None:
     """inner = outer for every parameter (src/utils.py:223-226)."""
+    if _host_path(inner_model, outer_model):
+        with torch.no_grad():
+            for po, pi in zip(outer_model.parameters(), inner_model.parameters()):
+                pi.data.copy_(po.data.to(pi.device))
+        return
     dev = _inner_device(inner_model)
     m = outer_mirror(outer_model, dev if dev.type != "cpu" else None)
     m.copy_to_inner(list(inner_model.parameters()))

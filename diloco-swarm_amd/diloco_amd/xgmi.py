@@ -72,13 +72,19 @@ class PeerMap:
             for q, info in enumerate(everyone):
                 if q == self.rank:
                     continue
+                # tensors of one peer that live in the same allocation (e.g. θ and the wire
+                # from one caching-allocator segment) share its IPC handle: open it once
+                seen: Dict[bytes, int] = {}
                 for k in self.names:
                     handle, off = info["bufs"][k]
-                    base = ctypes.c_void_p()
-                    _lib.call("dl_ipc_open", ctypes.create_string_buffer(handle, len(handle)),
-                              ctypes.byref(base))
-                    self._opened.append(base.value)
-                    self.ptrs[k][q] = base.value + off
+                    if handle not in seen:
+                        base = ctypes.c_void_p()
+                        _lib.call("dl_ipc_open",
+                                  ctypes.create_string_buffer(handle, len(handle)),
+                                  ctypes.byref(base))
+                        self._opened.append(base.value)
+                        seen[handle] = base.value
+                    self.ptrs[k][q] = seen[handle] + off
         except _lib.DilocoHipError as e:
             err = f"opening a peer's buffer failed: {e}"
         # second agreement: every rank mapped every peer, or every rank gives up together

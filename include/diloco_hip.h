@@ -16,8 +16,8 @@
  *   - A "packed" buffer holds the tree's tensors back to back in parameters() order, each
  *     segment starting at a multiple of DL_ALIGN_ELEMS elements; padding is never written.
  *   - "bucket" selects one bucket of the plan; DL_ALL_BUCKETS (-1) selects the whole tree.
- *   - All kernels are stream-ordered on the hipStream_t passed in; nothing synchronises the
- *     host except dl_tree_bind (once per pointer-set change).
+ *   - All kernels are stream-ordered on the hipStream_t passed in; no entry point
+ *     synchronises the host with a stream (dl_tree_bind is asynchronous too).
  */
 #ifndef DILOCO_HIP_H
 #define DILOCO_HIP_H
@@ -91,8 +91,12 @@ DL_API int dl_tree_seg_off(dl_tree_t tree, int64_t* seg_off /* n_seg+1 */);
 DL_API int dl_tree_bucket_chunks(dl_tree_t tree, int32_t bucket, int32_t* chunk_begin,
                                  int32_t* chunk_end);
 /* Upload the device addresses of the n_seg tensors of one slot (e.g. inner params, grads).
- * fp32 tensors, contiguous; a 16-B-misaligned address takes the scalar path. Synchronises
- * `stream` once (pointer sets change rarely; call again only when addresses change). */
+ * fp32 tensors, contiguous; a 16-B-misaligned address takes the scalar path. Stream-ordered
+ * on `stream` and asynchronous for the host: the n_seg addresses are staged in a ring of
+ * pinned slots and expanded into the slot's per-chunk table by a kernel, so rebinding grads
+ * that torch reallocated (zero_grad(set_to_none=True) before every inner step,
+ * src/train.py:164) costs no host synchronisation. Kernels queued on `stream` before the
+ * call still see the previous table; kernels on other streams must be ordered by the caller. */
 DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, int32_t n,
                         dl_stream_t stream);
 /* Launch shape of every walker kernel on this tree: max_blocks caps the grid (0 = one
@@ -226,6 +230,17 @@ DL_API int dl_reduce_scatter(const void* send, void* recv, int64_t recv_count, i
 /* recv[r*send_count : (r+1)*send_count) <- rank r's send[0:send_count) */
 DL_API int dl_all_gather(const void* send, void* recv, int64_t send_count, int32_t dtype,
                          dl_comm_t comm, dl_stream_t stream);
+/* Point-to-point, the payload leg of the device pipeline transport:
+ * replaces src/comm.py:38 `dist.send(tensor.to("cpu"), dst)` and src/comm.py:67
+ * `dist.recv(tensor, group)` (after the any-source header names the sender) with RCCL over
+ * xGMI on device buffers. A send and a receive on the same rank (or several transfers that
+ * must progress together) go between dl_group_start() and dl_group_end(). */
+DL_API int dl_send(const void* buf, int64_t count, int32_t dtype, int32_t peer, dl_comm_t comm,
+                   dl_stream_t stream);
+DL_API int dl_recv(void* buf, int64_t count, int32_t dtype, int32_t peer, dl_comm_t comm,
+                   dl_stream_t stream);
+DL_API int dl_group_start(void);
+DL_API int dl_group_end(void);
 
 /* ---- direct peer-access exchange (one node; SURVEY §8e alternative to RCCL) ----------------
  * IPC: dl_ipc_handle(ptr) -> the handle of the allocation holding ptr + ptr's byte offset in
@@ -250,6 +265,10 @@ DL_API int dl_enable_peer_access(int32_t peer);
  * re-reading their memory. Coarse-grained (hipMalloc / PyTorch) buffers are otherwise
  * coherent across GPUs only at the runtime's own synchronisation points. */
 DL_API int dl_sys_fence(dl_stream_t stream);
+/* dl_sys_fence that also records, per workgroup, the XCD it ran on (HW_REG_XCC_ID, 0..7) into
+ * the device array xcc[cap]; *grid = the workgroups launched (one per CU: multiProcessorCount).
+ * Lets a test prove that the fence reached every XCD. */
+DL_API int dl_sys_fence_census(uint32_t* xcc, int32_t cap, int32_t* grid, dl_stream_t stream);
 /* link probe: dst[i*bytes_each ...] <- srcs[i][0 .. bytes_each) for i < nsrc (<= 8), all
  * sources streamed at once by one kernel (measures per-link and aggregate peer read rates) */
 DL_API int dl_peer_gather(const uint64_t* srcs, int32_t nsrc, int64_t bytes_each, void* dst,
@@ -269,6 +288,13 @@ DL_API int dl_xgmi_delta_sgd(const uint64_t* inners, const uint64_t* thetas, int
                              int32_t rank, int64_t lo, int64_t len, float* mom, float lr,
                              float momentum, int32_t nesterov, int32_t first_step,
                              dl_stream_t stream);
+
+/* ---- calibration ------------------------------------------------------------------------
+ * dst[0:bytes) = src[0:bytes) with the segment walker's access shape (one 256-lane
+ * workgroup per 16 KiB, 4 float4 loads per lane before the stores); flags DL_TUNE_NT_LOADS =
+ * non-temporal loads and stores. bench.py times it in the same run as the outer step: the
+ * copy ceiling its roofline fractions are read against (not on the reference's path). */
+DL_API int dl_copy(const void* src, void* dst, int64_t bytes, int32_t flags, dl_stream_t stream);
 
 DL_API const char* dl_last_error(void);
 DL_API int dl_abi_version(void);

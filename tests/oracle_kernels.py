@@ -51,6 +51,9 @@ def _np(t):
 class OracleKernels:
     name = "oracle"
     default_device = torch.device("cpu")
+    # the engines treat host tensors as "device" tensors under this backend, so the mirror /
+    # engine orchestration runs on CPU (diloco_amd.utils.device_path)
+    accepts_host_tensors = True
 
     def check_device(self, device):
         assert device.type == "cpu"

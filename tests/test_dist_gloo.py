@@ -63,15 +63,16 @@ def _worker(rank, world, port, mode, num_stages, out):
     from diloco_amd.world import World
     from oracle_kernels import OracleKernels
 
-    kernels.set_default_kernels(OracleKernels())
+    if mode != "dropin_host":
+        kernels.set_default_kernels(OracleKernels())
     world_ = World.from_default_group(num_stages)
     dp_rank = world_.dp_ranks.index(rank)
     spec = get_tree("micro")
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
     rec = {}
-    if mode in ("dropin", "dropin_device", "dropin_deferred"):
-        from diloco_amd.utils import flush_outer_model
+    if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_host"):
+        from diloco_amd.utils import flush_outer_model, has_mirror
 
         deferred = mode == "dropin_deferred"
         inner = _micro_module(theta0, shapes)
@@ -80,8 +81,11 @@ def _worker(rank, world, port, mode, num_stages, out):
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
         assert type(opt).__name__ == "OuterSGD"
         from diloco_amd.utils import outer_mirror
-        assert type(outer_mirror(outer)).__name__ == (
-            "DeviceOuterMirror" if mode == "dropin_device" else "HostOuterMirror")
+        if mode == "dropin_host":  # the product's own host path: no kernel backend, no mirror
+            assert not has_mirror(outer)
+        else:
+            assert type(outer_mirror(outer)).__name__ == (
+                "DeviceOuterMirror" if mode == "dropin_device" else "HostOuterMirror")
         comm = TrainingComm(world_, (1, 1, 32), None)
         for s in range(1, MICRO_STEPS + 1):
             prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
@@ -120,6 +124,8 @@ def _worker(rank, world, port, mode, num_stages, out):
                 rec[f"theta_s{s}"] = host(outer.parameters())
                 rec[f"buf_s{s}"] = host(opt.state[p]["momentum_buffer"] for p in outer.parameters())
             rec[f"inner_s{s}"] = np.concatenate([p.detach().numpy().reshape(-1) for p in inner.parameters()])
+        if mode == "dropin_host":
+            assert not has_mirror(outer)  # every call took the reference's host semantics
     elif mode in ("engine", "engine_ar"):
         # engine: the default at n > 1, reduce-scatter -> shard SGD -> all-gather;
         # engine_ar: the replicated variant, all-reduce -> full SGD on every peer
@@ -251,7 +257,7 @@ def _run(mode, world, num_stages=1):
 
 
 @pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_deferred", "engine",
-                                  "engine_ar"])
+                                  "engine_ar", "dropin_host"])
 def test_two_peers_match_reference_bit_exact(mode):
     g = load_npz("micro_n2.npz")
     recs = _run(mode, 2)
@@ -268,7 +274,7 @@ def test_two_peers_match_reference_bit_exact(mode):
 
 
 @pytest.mark.parametrize("mode,world", [("dropin", 4), ("engine", 4), ("engine_ar", 4),
-                                        ("dropin", 8), ("engine", 8)])
+                                        ("dropin", 8), ("engine", 8), ("dropin_host", 4)])
 def test_four_and_eight_peers_match_reference_normwise(mode, world):
     """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""
     from diloco_amd.trees import get_tree
@@ -329,6 +335,19 @@ def test_device_p2p_transport_protocol():
     assert len(seen) == 10
     for src, root, i, tot in seen:
         assert src == root and tot == base + 32 * (1000 * src + i)
+
+
+def test_single_peer_host_dropin_matches_reference():
+    """--device cpu with one DP peer (BASELINE config #1's reference path at n = 1): the
+    product's host semantics, no kernel backend, byte-equal to micro_n1.npz."""
+    g = load_npz("micro_n1.npz")
+    rec = _run("dropin_host", 1)[0]
+    for s in (1, 2):
+        assert rec[f"delta_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        assert rec[f"avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()  # n = 1: no sync
+        for k in ("theta", "buf"):
+            assert rec[f"{k}_s{s}"].tobytes() == g[f"{k}_s{s}"].tobytes(), (k, s)
+        assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
 
 
 def test_sync_outputs_aggregates_like_reference():

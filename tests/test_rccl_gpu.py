@@ -257,3 +257,116 @@ def test_rccl_through_the_c_abi():
     g = load_npz("micro_n1.npz")
     for s in (1, 2):
         assert rec[f"cabi_theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+
+
+def _worker_t13b(rank, port, out):
+    """BASELINE configs #4/#5 at the full 1.3B tree through the bucketed collective paths over
+    a one-rank RCCL communicator (25 buckets of <= 256 MiB): the pipelined all-reduce path
+    (fp32 and bf16 wire) and the sharded reduce-scatter / all-gather path, each against the
+    same step without the collectives, 2 outer steps, on the device (torch.equal)."""
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from datetime import timedelta
+
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                            timeout=timedelta(seconds=120))
+    from diloco_amd import synth
+    from diloco_amd.outer import OuterSync
+    from diloco_amd.trees import get_tree
+
+    spec = get_tree("t1.3b")
+    shapes = [s for _, s in spec.params()]
+    rec = {}
+    cases = (("f32_pipelined", dict(wire_dtype=torch.float32, shard=False), dict(fuse_single=True)),
+             ("bf16_pipelined", dict(wire_dtype=torch.bfloat16, shard=False),
+              dict(wire_dtype=torch.bfloat16, fuse_single=False, tile_chunks=0)),
+             ("f32_sharded", dict(wire_dtype=torch.float32, shard=True), dict(fuse_single=True)))
+    for name, ka, kb in cases:
+        pa = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+        pb = [t.clone() for t in pa]
+        ea = OuterSync(pa, world_size=1, **ka)
+        eb = OuterSync(pb, world_size=1, **kb)
+        rec[f"{name}_buckets"] = np.array([ea.tree.n_buckets])
+        for s in (1, 2):
+            for e, ps in ((ea, pa), (eb, pb)):
+                th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+                synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in ps])
+            ea.step(pipeline=True)  # every bucket through RCCL (identity at one rank)
+            eb.step()
+        torch.cuda.synchronize()
+        ma, mb = ea.momentum_full(), eb.momentum_full()
+        rec[f"{name}_equal"] = np.array([
+            bool(torch.equal(ea.theta, eb.theta)) and bool(torch.equal(ma, mb))
+            and all(torch.equal(x, y) for x, y in zip(pa, pb))])
+        rec[f"{name}_sharded"] = np.array([ea.sharded])
+        ea.close()
+        eb.close()
+        del ea, eb, pa, pb, ma, mb
+        torch.cuda.empty_cache()
+    np.savez(os.path.join(out, "t13b.npz"), **rec)
+    dist.destroy_process_group()
+
+
+def test_rccl_t13b_bucketed_paths_match_single_pass():
+    out = tempfile.mkdtemp(prefix="dl_rccl_t13b_")
+    mp.spawn(_worker_t13b, args=(_free_port(), out), nprocs=1, join=True)
+    rec = dict(np.load(os.path.join(out, "t13b.npz")))
+    for name in ("f32_pipelined", "bf16_pipelined", "f32_sharded"):
+        assert rec[f"{name}_buckets"][0] == 25, name
+        assert rec[f"{name}_equal"][0], name
+    assert rec["f32_sharded_sharded"][0] and not rec["f32_pipelined_sharded"][0]
+
+
+def _worker_p2p(rank, port, out):
+    """The RCCL payload leg of the device pipeline transport (src/comm.py:33-38,64-69): framed
+    (8, 1024, 768) activations (dl_serialize on the GPU, fp32 and bf16 payloads) sent with
+    dl_send and received with dl_recv (one RCCL group: a send to self on a one-rank
+    communicator), on torch's communicator and on one the library creates."""
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from datetime import timedelta
+
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                            timeout=timedelta(seconds=120))
+    from diloco_amd import rccl
+    from diloco_amd.serializer import Serializer
+
+    dev = torch.device("cuda", 0)
+    shape = (8, 1024, 768)
+    g = torch.Generator().manual_seed(17)
+    acts = [torch.randn(shape, generator=g), torch.randn(shape, generator=g).to(torch.bfloat16)]
+    rec = {}
+    for name, comm in (("torch", rccl.Comm.from_process_group(None, dev)),
+                       ("own", rccl.Comm.create(1, 0, rccl.Comm.unique_id()))):
+        for i, a in enumerate(acts):
+            frame = Serializer(shape).serialize(a.to(dev), (3, 40 + i))
+            got = torch.full_like(frame, float("nan"))
+            with rccl.group():
+                comm.send(frame, 0)
+                comm.recv(got, 0)
+            torch.cuda.synchronize()
+            payload, meta = Serializer(shape).deserialize(got)
+            rec[f"{name}_{i}_meta"] = np.array(meta)
+            rec[f"{name}_{i}_bytes_equal"] = np.array([bool(torch.equal(
+                got.view(torch.int32)[1], frame.view(torch.int32)[1])) and bool(torch.equal(
+                    got[0].flatten()[:2], frame[0].flatten()[:2]))])
+            rec[f"{name}_{i}_payload"] = np.array([bool(torch.equal(payload.cpu(), a.float()))])
+        comm.close()
+    np.savez(os.path.join(out, "p2p.npz"), **rec)
+    dist.destroy_process_group()
+
+
+def test_rccl_p2p_payload_leg_carries_serialized_frames():
+    out = tempfile.mkdtemp(prefix="dl_rccl_p2p_")
+    mp.spawn(_worker_p2p, args=(_free_port(), out), nprocs=1, join=True)
+    rec = dict(np.load(os.path.join(out, "p2p.npz")))
+    for name in ("torch", "own"):
+        for i in range(2):
+            assert rec[f"{name}_{i}_meta"].tolist() == [3, 40 + i]
+            assert rec[f"{name}_{i}_bytes_equal"][0] and rec[f"{name}_{i}_payload"][0], (name, i)
