@@ -93,13 +93,14 @@ def setup_dist(n_gpus):
 
 
 def build(spec, dev, rank, wire, cap, fuse=False, shard=None, exchange="rccl", tile=None,
-          group=None):
+          group=None, keep_wire=False):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree_device(spec, dev)
     params = [t.view(s) for t, s in zip(theta0, shapes)]
     eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=wire,
                     bucket_cap_elems=cap, fuse_single=fuse, shard=shard, exchange=exchange,
-                    group=group, **({} if tile is None else {"tile_chunks": tile}))
+                    group=group, keep_wire=keep_wire,
+                    **({} if tile is None else {"tile_chunks": tile}))
     # inner = θ_0 + this rank's noise (stands in for H inner steps)
     synth.inner_tree_device([p.view(-1) for p in params], 1, rank, out=[p.view(-1) for p in params])
     return eng
@@ -188,11 +189,11 @@ def with_copy_ceiling(entry, ceiling_gbs):
 
 
 def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loops=True,
-             shard=None, exchange="rccl", tile=None, cold=False):
+             shard=None, exchange="rccl", tile=None, cold=False, keep_wire=False):
     """Timed region (K outer steps, nothing else on the stream), then an instrumented pass of
     K more steps with HIP events between the kernels on the stream they run on (events in the
     timed region would cost the step ~35 us each), then the same kernels back to back."""
-    eng = build(spec, dev, rank, wire, cap, fuse, shard, exchange, tile)
+    eng = build(spec, dev, rank, wire, cap, fuse, shard, exchange, tile, keep_wire=keep_wire)
     P = spec.total()
     for _ in range(max(warmup, 1)):  # >= 1: the timed steps run the steady-state SGD mode
         eng.step()
@@ -205,11 +206,14 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
     wb = 2 if wire == torch.bfloat16 else 4
     single = ws == 1
     # instrumented pass (the kernels in their in-step context)
+    # the kernels are timed on the stream they run on: eng._step launches on the current
+    # stream (eng.step would hop to the engine's side stream and back, ~20-30 us of
+    # cross-stream latency inside the events)
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     for e in ev:
         e[0].record()
         if single and fuse:
-            eng.step()
+            eng._step(None)
             e[1].record()
         elif single:
             eng.pseudo_gradient()
@@ -230,7 +234,9 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
            "value_aggregate": ws * 4.0 * P / (dt / steps) / 1e9,
            "wire": "bf16" if wire == torch.bfloat16 else "f32",
            "tile_chunks": eng.tile_chunks if single and not fuse else None,
-           "variant": ("one replica: dl_delta_sgd (one pass)" if single and fuse
+           "variant": ("one replica: dl_delta_pack_sgd (one pass, pseudo-gradient kept in the "
+                       "packed wire)" if single and fuse and keep_wire
+                       else "one replica: dl_delta_sgd (one pass, no wire)" if single and fuse
                        else "direct exchange from the peers' inner arenas (dl_xgmi_delta_sgd)"
                        if eng.xgmi_inner
                        else ("one replica: dl_delta_pack -> dl_unpack_sgd"
@@ -239,9 +245,11 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
                        else "direct peer-access exchange (IPC, dl_xgmi_reduce_sgd)" if eng.xgmi
                        else "reduce_scatter -> shard SGD -> all_gather" if eng.sharded
                        else "all_reduce -> replicated SGD")}
+    fused_name = "delta_pack_sgd" if keep_wire else "delta_sgd"
+    # read θ, inner, buf; write θ, buf, inner (+ the wire)
+    fused_bytes = (24 + (wb if keep_wire else 0)) * P
     if single and fuse:
-        b = 24 * P  # read θ, inner, buf; write θ, buf, inner
-        res["kernels"] = {"delta_sgd": kernel_entry(b, first, pmc.get("delta_sgd"))}
+        res["kernels"] = {fused_name: kernel_entry(fused_bytes, first, pmc.get(fused_name))}
     elif single:
         res["kernels"] = {
             "delta_pack": kernel_entry((8 + wb) * P, first, pmc.get("delta_pack")),
@@ -254,11 +262,12 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         # the events), as after H inner steps in training
         scr = Scrubber(dev)
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        tiled = not fuse and eng.tile_chunks
         for e in ev:
             scr()
             e[0].record()
-            if fuse:
-                eng.step()
+            if fuse or tiled:  # the step as the engine runs it, on this stream
+                eng._step(None)
                 e[1].record()
             else:
                 eng.pseudo_gradient()
@@ -275,7 +284,9 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
                        "note": "Infinity Cache scrubbed before each step (512 MiB copy, "
                                "outside the events); step = the kernels' event span"}
         if fuse:
-            res["cold"]["kernels"] = {"delta_sgd": kernel_entry(24 * P, c_first)}
+            res["cold"]["kernels"] = {fused_name: kernel_entry(fused_bytes, c_first)}
+        elif tiled:
+            res["cold"]["kernels"] = {}  # tile-interleaved launches: the step only
         else:
             res["cold"]["kernels"] = {
                 "delta_pack": kernel_entry((8 + wb) * P, c_first),
@@ -292,7 +303,10 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         e1.synchronize()
         return e0.elapsed_time(e1) / reps
 
-    if b2b_loops and not (eng.sharded or eng.xgmi):
+    if b2b_loops and single and fuse:
+        res["kernels_b2b"] = {fused_name: kernel_entry(fused_bytes,
+                                                        b2b(lambda: eng._step(None)))}
+    elif b2b_loops and not (eng.sharded or eng.xgmi):
         res["kernels_b2b"] = {"delta_pack": kernel_entry((8 + wb) * P, b2b(eng.pseudo_gradient)),
                               "unpack_sgd": kernel_entry((wb + 20) * P, b2b(eng.apply))}
     if single:
@@ -947,9 +961,9 @@ def _guard(fn, *a, **k):
 
 
 def _brief(r):
-    keep = ("value", "value_aggregate", "ms_per_step", "roofline", "kernels", "buckets", "params",
-            "wire", "variant", "wire_bytes_per_param", "bus_bytes_per_step", "tile_chunks",
-            "cold")
+    keep = ("value", "value_aggregate", "ms_per_step", "roofline", "kernels", "kernels_b2b",
+            "buckets", "params", "wire", "variant", "wire_bytes_per_param", "bus_bytes_per_step",
+            "tile_chunks", "cold")
     return {k: r[k] for k in keep if k in r}
 
 
@@ -1203,8 +1217,10 @@ def main():
     # (tools/tile_ab.py) and is what the T1.3B leg below runs (OuterSync's default tile)
     fallback = None
     try:
-        main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap,
-                            b2b_loops=not a.no_b2b, tile=0, cold=not a.only_headline)
+        # N = 1: the one-replica step in one pass, pseudo-gradient kept (dl_delta_pack_sgd)
+        main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap, fuse=ws == 1,
+                            b2b_loops=not a.no_b2b, tile=0, cold=not a.only_headline,
+                            keep_wire=True)
     except Exception as e:  # N > 1: the replicated all-reduce step still gives the driver a line
         if ws == 1:
             raise
@@ -1245,10 +1261,13 @@ def main():
         "dtype": "f32" if a.wire == "f32" else "f32 (bf16 wire)",
         "data": "synthetic (counter-based GPT-2-shaped tree, SURVEY.md §8d)",
         "config": {
-            "workload": (f"DiLoCo outer step, {spec.name} tree per rank: delta_pack -> "
-                         + ("RCCL reduce_scatter -> shard_sgd (1/n of θ, momentum) -> RCCL "
-                            "all_gather(θ) -> scatter to inner (bucketed, pipelined)"
-                            if ws > 1 else "unpack_sgd (+copy to inner)")),
+            "workload": (f"DiLoCo outer step, {spec.name} tree per rank: "
+                         + ("delta_pack -> RCCL reduce_scatter -> shard_sgd (1/n of θ, "
+                            "momentum) -> RCCL all_gather(θ) -> scatter to inner (bucketed, "
+                            "pipelined)" if ws > 1 else
+                            "delta + pack (wire = outer.grad) + Nesterov SGD + copy to inner "
+                            "in one pass (dl_delta_pack_sgd; no exchange at one replica, "
+                            "src/comm.py:118-119)")),
             "tree": spec.name, "params": main_res["params"], "tensors": main_res["tensors"],
             "wire": a.wire, "buckets": main_res["buckets"], "chunks": main_res["chunks"],
             "parallelism": f"dp{ws}",
@@ -1290,6 +1309,13 @@ def main():
 
     if not a.only_headline:
         if ws == 1:
+            # BASELINE config #2's two kernels as separate launches (delta_pack -> unpack_sgd,
+            # whole-range: per-kernel warm / cold / back-to-back figures) and the cache-blocked
+            # two-kernel step (OuterSync's tiles), then the one pass without the wire
+            leg(f"{spec.name}_two_kernel", run_tree, spec, dev, ws, rank, a.steps, a.warmup,
+                wire, cap, False, True, None, "rccl", 0, True)
+            leg(f"{spec.name}_two_kernel_tiled", run_tree, spec, dev, ws, rank, a.steps,
+                a.warmup, wire, cap, False, False, None, "rccl", None, True)
             leg(f"{spec.name}_fused_single", run_tree, spec, dev, ws, rank, a.steps, a.warmup,
                 wire, cap, True, True, None, "rccl", None, True)
         if a.extra_tree != "none" and a.extra_tree != a.tree:

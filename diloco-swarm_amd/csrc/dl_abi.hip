@@ -432,6 +432,23 @@ DL_API int dl_delta_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_sgd");
 }
 
+DL_API int dl_delta_pack_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer, void* wire,
+                             int32_t wire_dtype, float* mom, float lr, float momentum,
+                             int32_t nesterov, int32_t first_step, dl_stream_t s) {
+  dl::Launch L;
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack_sgd", kAutoUnpackSgd));
+  DL_TRY(check_slot(t, inner_slot, "dl_delta_pack_sgd"));
+  DL_TRY(check_packed(outer, "dl_delta_pack_sgd", "outer"));
+  DL_TRY(check_packed(wire, "dl_delta_pack_sgd", "wire"));
+  DL_TRY(check_dtype(wire_dtype, "dl_delta_pack_sgd"));
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_delta_pack_sgd", "momentum"));
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_delta_pack_sgd: Nesterov momentum requires a momentum");
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_delta_pack_sgd(L, inner_slot, outer, wire, wire_dtype, mom, a);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_pack_sgd");
+}
+
 // a2 -> (one peer: the exchange is the identity, src/comm.py:118-119) -> a3-a5, cache-blocked:
 // the tree is walked in tiles of tile_chunks chunks and each tile runs dl_delta_pack then
 // dl_unpack_sgd, so the wire and θ bytes the pack just touched are re-read by the unpack from

@@ -66,6 +66,8 @@ hipError_t launch_unpack_avg(const Launch& L, const void* wire, int wire_dtype, 
 hipError_t launch_unpack_sgd(const Launch& L, const void* wire, int wire_dtype, int divisor,
                              float* outer, float* mom, SgdArgs a, int inner_slot);
 hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float* mom, SgdArgs a);
+hipError_t launch_delta_pack_sgd(const Launch& L, int inner_slot, float* outer, void* wire,
+                                 int wire_dtype, float* mom, SgdArgs a);
 hipError_t launch_shard_sgd(const void* wire, int wire_dtype, int divisor, float* outer, float* mom,
                             int64_t n, SgdArgs a, hipStream_t s);
 hipError_t launch_delta_q8(const Launch& L, int inner_slot, const float* outer, uint8_t* slots);

@@ -221,6 +221,83 @@ struct DeltaSgd {
   }
 };
 
+// a2+a3+a4+a5 at ONE peer with the pseudo-gradient kept: dl_delta_sgd that also stores the
+// packed wire (outer.grad of src/utils.py:221, the reference's observable .grad after the
+// step). g = θ - inner; wire = W(g); the SGD consumes the value on the wire (a bf16 wire
+// rounds it first, as dl_unpack_sgd would read it back); θ, buf, inner <- new values.
+// 28 B/param (fp32 wire; 24 on the first step) instead of 12 + 24 for dl_delta_pack +
+// dl_unpack_sgd: the wire and θ are not read back. Bit-identical to that pair.
+template <typename W, int MODE>
+struct DeltaPackSgd {
+  float* outer;
+  W* wire;
+  float* mom;
+  SgdArgs a;
+  int inner_slot;
+  static __device__ __forceinline__ float on_wire(float g) {
+    if constexpr (sizeof(W) == 2) return bf2f(f2bf(g));
+    else return g;
+  }
+  template <bool NTL, bool NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
+    float* th = outer + ck.poff;
+    float* mb = mom + ck.poff;
+    W* w = wire + ck.poff;
+    if (aligned16(in)) {
+      const int nv = ck.len >> 2;
+      float4 x[kUnroll], t[kUnroll], m[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int v = u * kThreads + tid;
+        if (v < nv) {
+          t[u] = ldf4<NTL>(th, v);
+          x[u] = ldf4<NTL>(in, v);
+          if (MODE == 2) m[u] = ldf4<NTL>(mb, v);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int v = u * kThreads + tid;
+        if (v < nv) {
+          float4 g = sub4(t[u], x[u]);
+          WireIO<W>::template st4<NTS>(w, v, g);
+          g = make_float4(on_wire(g.x), on_wire(g.y), on_wire(g.z), on_wire(g.w));
+          sgd1<MODE>(g.x, m[u].x, t[u].x, a);
+          sgd1<MODE>(g.y, m[u].y, t[u].y, a);
+          sgd1<MODE>(g.z, m[u].z, t[u].z, a);
+          sgd1<MODE>(g.w, m[u].w, t[u].w, a);
+          stf4<NTS>(th, v, t[u]);
+          if (MODE != 0) stf4<NTS>(mb, v, m[u]);
+          stf4<NTS>(in, v, t[u]);
+        }
+      }
+      const int i = (nv << 2) + tid;
+      if (i < ck.len) {
+        const float g0 = th[i] - in[i];
+        WireIO<W>::st1(w, i, g0);
+        const float g = on_wire(g0);
+        float b = (MODE == 2) ? mb[i] : 0.f, t1 = th[i];
+        sgd1<MODE>(g, b, t1, a);
+        th[i] = t1;
+        if (MODE != 0) mb[i] = b;
+        in[i] = t1;
+      }
+    } else {
+      for (int i = tid; i < ck.len; i += kThreads) {
+        const float g0 = th[i] - in[i];
+        WireIO<W>::st1(w, i, g0);
+        const float g = on_wire(g0);
+        float b = (MODE == 2) ? mb[i] : 0.f, t1 = th[i];
+        sgd1<MODE>(g, b, t1, a);
+        th[i] = t1;
+        if (MODE != 0) mb[i] = b;
+        in[i] = t1;
+      }
+    }
+  }
+};
+
 // per-tensor fp32 -> packed W
 template <typename W>
 struct Gather {
@@ -498,6 +575,21 @@ hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float
   if (a.momentum == 0.f) return run(L, DeltaSgd<0>{outer, mom, a, inner_slot});
   if (a.first) return run(L, DeltaSgd<1>{outer, mom, a, inner_slot});
   return run(L, DeltaSgd<2>{outer, mom, a, inner_slot});
+}
+
+template <typename W>
+static hipError_t delta_pack_sgd_t(const Launch& L, int inner_slot, float* outer, W* wire,
+                                   float* mom, SgdArgs a) {
+  if (a.momentum == 0.f) return run(L, DeltaPackSgd<W, 0>{outer, wire, mom, a, inner_slot});
+  if (a.first) return run(L, DeltaPackSgd<W, 1>{outer, wire, mom, a, inner_slot});
+  return run(L, DeltaPackSgd<W, 2>{outer, wire, mom, a, inner_slot});
+}
+
+hipError_t launch_delta_pack_sgd(const Launch& L, int inner_slot, float* outer, void* wire,
+                                 int wire_dtype, float* mom, SgdArgs a) {
+  if (wire_dtype == DL_BF16)
+    return delta_pack_sgd_t(L, inner_slot, outer, static_cast<bf16_t*>(wire), mom, a);
+  return delta_pack_sgd_t(L, inner_slot, outer, static_cast<float*>(wire), mom, a);
 }
 
 hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype) {

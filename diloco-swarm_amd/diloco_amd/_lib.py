@@ -52,6 +52,9 @@ SIGNATURES = {
         [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _i32, _vp],
     ),
     "dl_delta_sgd": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _f32, _f32, _i32, _i32, _vp]),
+    "dl_delta_pack_sgd": (
+        ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _vp, _f32, _f32, _i32, _i32, _vp],
+    ),
     "dl_pack_sgd_tiled": (
         ctypes.c_int,
         [_vp, _i32, _i32, _vp, _vp, _i32, _vp, _f32, _f32, _i32, _i32, _i32, _vp],

@@ -72,6 +72,13 @@ class HipKernels:
         _lib.call("dl_delta_sgd", tree.handle, bucket, inner_slot, theta.data_ptr(), _ptr(mom),
                   float(lr), float(momentum), int(nesterov), int(first), _s(theta))
 
+    def delta_pack_sgd(self, tree, bucket, inner_slot, theta, wire, mom, lr, momentum, nesterov,
+                       first) -> None:
+        """One peer, one pass: delta + SGD + copy-back, the pseudo-gradient kept in `wire`."""
+        _lib.call("dl_delta_pack_sgd", tree.handle, bucket, inner_slot, theta.data_ptr(),
+                  wire.data_ptr(), wire_code(wire.dtype), _ptr(mom), float(lr), float(momentum),
+                  int(nesterov), int(first), _s(theta))
+
     def pack_sgd_tiled(self, tree, bucket, inner_slot, theta, wire, mom, lr, momentum,
                        nesterov, first, tile_chunks) -> None:
         """One peer: delta_pack then unpack_sgd (divisor 1) tile by tile (Infinity-Cache

@@ -10,7 +10,9 @@ One `OuterSync` per DP replica (one process per GPU). It performs, for the whole
 
 Exchange variants, all bucketed and pipelined across buckets:
   one replica        dl_delta_sgd: delta, SGD and copy-back in one pass (24 B/param);
-                     fuse_single=False keeps BASELINE config #2's dl_delta_pack -> dl_unpack_sgd
+                     keep_wire=True: dl_delta_pack_sgd, the same pass also storing the packed
+                     pseudo-gradient (outer.grad; 28 B/param); fuse_single=False: the
+                     two-kernel dl_delta_pack -> dl_unpack_sgd pipeline, tile by tile
   sharded            (default for n > 1 with the fp32 wire) RCCL reduce-scatter ->
                      dl_shard_sgd on this peer's 1/n (θ and momentum shards) -> RCCL all-gather
                      of θ -> dl_scatter; HBM 20 + 20/n B/param, momentum 4P/n
@@ -37,12 +39,13 @@ from .kernels import Q8_SLOT, default_kernels
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER
 
 ALL = _lib.ALL_BUCKETS
-# Tile of dl_pack_sgd_tiled: 4096 chunks = 16 Mi elements, 64 MiB per stream. Measured
-# (tools/tile_ab.py, profiles/r01_tile_ab_*.json): T1.3B one-replica step 8.25 -> 7.55 ms
-# (the step re-reads wire and θ of the tile from the Infinity Cache); T125 unchanged (0.694
-# vs 0.697 ms: its whole-range step already reuses the cache across the step boundary).
-# Smaller tiles lose: every extra launch boundary costs ≈ 2 µs (256-chunk tiles: 1.18 ms).
-DEFAULT_TILE_CHUNKS = 4096
+# Tile of dl_pack_sgd_tiled: 8192 chunks = 32 Mi elements, 128 MiB per stream (wire + θ of a
+# tile = 256 MiB, the Infinity Cache). Measured cold -- the Infinity Cache scrubbed before
+# every step, as after H inner steps (tools/cold_sweep.py, profiles/r02_cold_sweep_*.json):
+# T1.3B 8.01 ms whole-range, 7.33 ms at 4096, 6.96 ms at 8192 (the unpack re-reads the tile's
+# wire and θ from the Infinity Cache); T125 0.723 / 0.742 / 0.709 ms. Smaller tiles lose:
+# every extra launch boundary costs ≈ 2 µs (1024-chunk tiles: T125 0.876 ms).
+DEFAULT_TILE_CHUNKS = 8192
 
 
 def pipelined_buckets(n_buckets: int, pack: Callable[[int], None],
@@ -93,6 +96,7 @@ class OuterSync:
         rank: Optional[int] = None,
         exchange: str = "rccl",
         tile_chunks: int = DEFAULT_TILE_CHUNKS,
+        keep_wire: bool = False,
     ):
         self._objs = list(params)  # the caller's objects (exchange="xgmi_inner" relays them)
         self.params: List[torch.Tensor] = [p.data if isinstance(p, torch.nn.Parameter) else p
@@ -107,6 +111,9 @@ class OuterSync:
         self.wire_dtype = wire_dtype
         # one replica: delta + SGD + copy-back in one pass (dl_delta_sgd), no wire round trip
         self.fuse_single = bool(fuse_single)
+        # ... and with keep_wire, store the pseudo-gradient into the wire in the same pass
+        # (dl_delta_pack_sgd): the reference's outer.grad stays observable after the step
+        self.keep_wire = bool(keep_wire)
         # one replica, two-kernel pipeline: pack/step tile by tile (dl_pack_sgd_tiled) so the
         # step re-reads the wire and θ from the Infinity Cache; 0 = whole-range launches
         if tile_chunks < 0:
@@ -397,8 +404,12 @@ class OuterSync:
         elif pipeline:
             pipelined_buckets(self.tree.n_buckets, self.pseudo_gradient,
                               lambda b: self.all_reduce(b, async_op=True), self.apply)
-        elif self.fuse_single:
+        elif self.fuse_single and self.keep_wire:
             # src/comm.py:118-119: one peer -> no all-reduce and no division
+            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+            self.k.delta_pack_sgd(self.tree, ALL, SLOT_INNER, self.theta, self.wire, self.mom,
+                                  self.lr, self.momentum, self.nesterov, self.steps_done == 0)
+        elif self.fuse_single:
             self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.delta_sgd(self.tree, ALL, SLOT_INNER, self.theta, self.mom, self.lr,
                              self.momentum, self.nesterov, self.steps_done == 0)

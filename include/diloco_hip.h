@@ -147,6 +147,17 @@ DL_API int dl_delta_sgd(dl_tree_t tree, int32_t bucket, int32_t inner_slot, floa
                         float* mom_packed, float lr, float momentum, int32_t nesterov,
                         int32_t first_step, dl_stream_t stream);
 
+/* a2+a3+a4+a5 at ONE peer, keeping the pseudo-gradient: dl_delta_sgd that also writes the
+ * packed wire (outer.grad of src/utils.py:221, as dl_delta_pack would):
+ *   g = θ - inner[seg][j]; wire[k] = g (bf16 wire: RNE, and the SGD uses the rounded value);
+ *   SGD as dl_unpack_sgd (divisor 1); θ and inner[seg][j] <- new θ
+ * One pass: 28 B/param (fp32 wire; 24 on the first step) instead of 36 for dl_delta_pack +
+ * dl_unpack_sgd, bit-identical to that pair (wire included). */
+DL_API int dl_delta_pack_sgd(dl_tree_t tree, int32_t bucket, int32_t inner_slot,
+                             float* outer_packed, void* wire, int32_t wire_dtype,
+                             float* mom_packed, float lr, float momentum, int32_t nesterov,
+                             int32_t first_step, dl_stream_t stream);
+
 /* a2 -> a3 -> a4 -> a5 at ONE peer as the two-kernel pipeline (dl_delta_pack then
  * dl_unpack_sgd with divisor 1; src/utils.py:221, src/comm.py:118-119, src/train.py:267,
  * src/utils.py:226), cache-blocked: the bucket's chunk range is walked in tiles of

@@ -97,6 +97,13 @@ class OracleKernels:
         self.unpack_sgd(tree, bucket, wire, 1, theta, mom, lr, momentum, nesterov, first,
                         inner_slot)
 
+    def delta_pack_sgd(self, tree, bucket, inner_slot, theta, wire, mom, lr, momentum,
+                       nesterov, first):
+        # one pass on the device; restated as the pair it is bit-identical to
+        self.delta_pack(tree, bucket, inner_slot, theta, wire)
+        self.unpack_sgd(tree, bucket, wire, 1, theta, mom, lr, momentum, nesterov, first,
+                        inner_slot)
+
     def delta_sgd(self, tree, bucket, inner_slot, theta, mom, lr, momentum, nesterov, first):
         for i in tree.segs(bucket):
             th = self._seg(tree, theta, i).copy()

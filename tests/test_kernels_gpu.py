@@ -299,6 +299,69 @@ def test_fused_single_peer_ragged_vs_two_kernel_path(momentum, nesterov):
 
 @pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("momentum,nesterov", [(0.9, True), (0.9, False), (0.0, False)])
+@pytest.mark.parametrize("misaligned", [False, True])
+def test_delta_pack_sgd_equals_two_kernel_pair(wire, momentum, nesterov, misaligned):
+    """dl_delta_pack_sgd (one pass, the pseudo-gradient kept in the wire) is bit-identical to
+    dl_delta_pack -> dl_unpack_sgd: θ, momentum, inner AND the wire, ragged tensors (tails,
+    empty), 4-B-aligned storage (scalar path), fp32 and bf16 wires, every SGD mode."""
+    g0 = torch.Generator().manual_seed(23)
+    host = [torch.randn(n, generator=g0) for n in RAGGED]
+
+    def place():
+        if not misaligned:
+            return [h.to(DEV) for h in host]
+        base = torch.empty(sum(RAGGED) + len(RAGGED), device=DEV)
+        out, o = [], 1
+        for h in host:
+            out.append(base[o:o + h.numel()])
+            out[-1].copy_(h)
+            o += h.numel() + 1
+        return out
+
+    pa, pb = place(), place()
+    ea = OuterSync(pa, momentum=momentum, nesterov=nesterov, world_size=1, wire_dtype=wire,
+                   fuse_single=True, keep_wire=True)
+    eb = OuterSync(pb, momentum=momentum, nesterov=nesterov, world_size=1, wire_dtype=wire,
+                   fuse_single=False, tile_chunks=0)
+    iview = torch.int16 if wire == torch.bfloat16 else torch.int32
+    for _ in range(3):
+        noise = [torch.randn(n, generator=g0).to(DEV) * 1e-3 for n in RAGGED]
+        for p, q, z in zip(pa, pb, noise):
+            p.add_(z)
+            q.add_(z)
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(ea.theta.view(torch.int32), eb.theta.view(torch.int32))
+        assert torch.equal(ea.wire.view(iview), eb.wire.view(iview))
+        if momentum:
+            assert torch.equal(ea.mom.view(torch.int32), eb.mom.view(torch.int32))
+        for p, q in zip(pa, pb):
+            assert p.cpu().numpy().tobytes() == q.cpu().numpy().tobytes()
+
+
+def test_delta_pack_sgd_micro_matches_reference():
+    """The one-pass step with the wire kept reproduces the reference's outer steps AND its
+    outer.grad (the wire holds delta_s{s}_r0 after step s), micro tree, n = 1."""
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    params = [t.clone().view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
+    e = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True)
+    g = load_npz("micro_n1.npz")
+    for s in (1, 2):
+        th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+        synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+        e.step()
+        torch.cuda.synchronize()
+        assert np.concatenate(_host(e.unpacked(e.wire))).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        assert np.concatenate(_host(e.unpacked(e.theta))).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert np.concatenate(_host(e.unpacked(e.mom))).tobytes() == g[f"buf_s{s}"].tobytes()
+        assert np.concatenate(_host(params)).tobytes() == g[f"theta_s{s}"].tobytes()
+    e.close()
+
+
+@pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("momentum,nesterov", [(0.9, True), (0.9, False), (0.0, False)])
 def test_tiled_pack_sgd_equals_whole_range_launches(wire, momentum, nesterov):
     """dl_pack_sgd_tiled (Infinity-Cache-blocked delta_pack -> unpack_sgd) is bit-identical to
     the two whole-range launches for tiles of 1, 3 and 7 chunks (tiles cut tensors and end
@@ -382,15 +445,22 @@ def test_t13b_full_size_sampled_tensors_vs_oracle_and_fused():
     shapes = [s for _, s in spec.params()]
     pa = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
     pb = [t.clone() for t in pa]
+    pc = [t.clone() for t in pa]
     ea = OuterSync(pa, world_size=1, fuse_single=False)
     eb = OuterSync(pb, world_size=1, fuse_single=True)
-    for e, ps in ((ea, pa), (eb, pb)):
+    ec = OuterSync(pc, world_size=1, fuse_single=True, keep_wire=True)
+    for e, ps in ((ea, pa), (eb, pb), (ec, pc)):
         th = [t.reshape(-1) for t in e.unpacked(e.theta)]
         synth.inner_tree_device(th, 1, 0, out=[p.view(-1) for p in ps])
         e.step()
     torch.cuda.synchronize()
     assert torch.equal(ea.theta, eb.theta) and torch.equal(ea.mom, eb.mom)
+    assert torch.equal(ea.theta, ec.theta) and torch.equal(ea.mom, ec.mom)
+    assert torch.equal(ea.wire, ec.wire)  # the kept pseudo-gradient == dl_delta_pack's
     assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    assert all(torch.equal(x, y) for x, y in zip(pa, pc))
+    ec.close()
+    del ec, pc
     numels, init = spec.numels(), spec.init_spec()
     for t in (0, 2, 4, len(numels) - 1):
         th0 = synth.values(synth.OUTER_SEED, t, numels[t], *init[t])

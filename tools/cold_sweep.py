@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""Cold A/B of the product kernels (the state a DiLoCo outer step runs in: H inner steps have
+evicted the Infinity Cache): the 256 MiB Infinity Cache is scrubbed (a 512 MiB dl_copy) before
+every timed launch, variants interleaved round by round in one process (cdna_hip_programming.md
+§5.4 rule 24); median / min ms and GB/s of algorithmic bytes.
+
+    python tools/cold_sweep.py [--tree t125] [--rounds 11] [--out x.json] [--what flags,tiles]
+
+flags : dl_tree_tune launch policy (NT loads / NT stores) of dl_delta_pack, dl_unpack_sgd,
+        dl_delta_sgd one launch over the whole tree each
+tiles : the one-replica two-kernel step (dl_pack_sgd_tiled) at tile sizes 0 (whole-range
+        launches), 1024 ... 16384 chunks, against the one-pass dl_delta_sgd
+"""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "diloco-swarm_amd"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import torch  # noqa: E402
+
+from diloco_amd import _lib, synth  # noqa: E402
+from diloco_amd.outer import OuterSync  # noqa: E402
+from diloco_amd.trees import get_tree  # noqa: E402
+
+
+def timed_cold(fn, scrub):
+    scrub()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def summarize(ms, nbytes):
+    ms = sorted(ms)
+    med = ms[len(ms) // 2]
+    return {"med_ms": round(med, 4), "min_ms": round(ms[0], 4),
+            "med_GBs": round(nbytes / med / 1e6, 1), "best_GBs": round(nbytes / ms[0] / 1e6, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tree", default="t125")
+    ap.add_argument("--rounds", type=int, default=11)
+    ap.add_argument("--what", default="flags,tiles")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from bench import Scrubber
+
+    dev = torch.device("cuda", 0)
+    spec = get_tree(a.tree)
+    P = spec.total()
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)]
+    synth.inner_tree_device([p.view(-1) for p in params], 1, 0, out=[p.view(-1) for p in params])
+    scrub = Scrubber(dev)
+    out = {"tree": a.tree, "params": P, "rounds": a.rounds}
+    what = a.what.split(",")
+    if "flags" in what:
+        two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
+        one = OuterSync(params, world_size=1, fuse_single=True)
+        two.step()
+        one.step()  # steady-state SGD mode from here on
+        kern = {"delta_pack": (two, two.pseudo_gradient, 12),
+                "unpack_sgd": (two, two.apply, 24),
+                "delta_sgd": (one, one.step, 24)}
+        flag_names = {1: "nt_loads", 3: "nt_loads+stores", 0: "plain", 2: "nt_stores"}
+        res = {(k, f): [] for k in kern for f in flag_names}
+        for _ in range(a.rounds):
+            for (k, f) in res:
+                eng, fn, _ = kern[k]
+                eng.tree.tune(0, f)
+                res[(k, f)].append(timed_cold(fn, scrub))
+        two.tree.tune(0, _lib.TUNE_AUTO)
+        one.tree.tune(0, _lib.TUNE_AUTO)
+        out["flags"] = {}
+        for (k, f), ms in res.items():
+            s = summarize(ms, kern[k][2] * P)
+            out["flags"].setdefault(k, {})[flag_names[f]] = s
+            print(f"{k:11s} {flag_names[f]:16s} med {s['med_ms']:.4f} ms {s['med_GBs']:7.1f} GB/s"
+                  f"  best {s['best_GBs']:7.1f}", flush=True)
+        two.close()
+        one.close()
+    if "tiles" in what:
+        engs = {}
+        for tile in (0, 1024, 2048, 4096, 8192, 16384):
+            engs[f"tile{tile}"] = OuterSync(params, world_size=1, fuse_single=False,
+                                            tile_chunks=tile)
+        engs["delta_sgd"] = OuterSync(params, world_size=1, fuse_single=True)
+        for e in engs.values():
+            e.step()
+        res = {k: [] for k in engs}
+        for _ in range(a.rounds):
+            for k, e in engs.items():
+                res[k].append(timed_cold(e.step, scrub))
+        out["tiles"] = {}
+        for k, ms in res.items():
+            s = summarize(ms, 4 * P)  # GB/s params reduced (the metric)
+            out["tiles"][k] = s
+            print(f"step {k:10s} med {s['med_ms']:.4f} ms {s['med_GBs']:7.1f} GB/s params reduced"
+                  f"  best {s['best_GBs']:7.1f}", flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

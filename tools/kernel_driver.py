@@ -31,6 +31,10 @@ def main():
     fused.step()
     for _ in range(reps):
         fused.step()
+    kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True)
+    kept.step()
+    for _ in range(reps):
+        kept.step()
     # one bucket each, so every launch covers the whole tree: the int8 wire kernels and the
     # sharded step's dl_shard_sgd (one replica: the shard is the whole bucket)
     q8 = OuterSync(params, world_size=1, wire_dtype=torch.int8, bucket_cap_elems=0)

@@ -18,7 +18,8 @@ from collections import defaultdict
 def short(name):
     # most specific first: k_flat<UnpackSgd...> is dl_shard_sgd, UnpackSgdQ8 is not UnpackSgd
     names = {"k_xgmi_reduce_sgd": "xgmi_reduce_sgd", "k_flat": "shard_sgd", "DeltaQ8": "delta_q8", "UnpackSgdQ8": "unpack_sgd_q8",
-             "k_q8_reduce": "q8_reduce", "DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd",
+             "k_q8_reduce": "q8_reduce", "DeltaPackSgd": "delta_pack_sgd",
+             "DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd",
              "UnpackAvg": "unpack_avg", "DeltaSgd": "delta_sgd", "Gather": "gather",
              "Scatter": "scatter", "k_fill_synth": "fill_synth"}
     if "k_xgmi_reduce_sgd" in name and ", true>" in name:
@@ -27,6 +28,7 @@ def short(name):
         if k in name:
             first = ((k in ("UnpackSgd", "k_flat") and ", 1>" in name)
                      or (k == "DeltaSgd" and "DeltaSgd<1>" in name)
+                     or (k == "DeltaPackSgd" and ", 1>" in name)
                      or (k == "UnpackSgdQ8" and "UnpackSgdQ8<1>" in name))
             return v + ("_first" if first else "")
     return None
