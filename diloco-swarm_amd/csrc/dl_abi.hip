@@ -297,7 +297,13 @@ DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t
   // table; the rewrite is ordered behind them.
   const int k = t->stage_next;
   t->stage_next = (k + 1) % kStageRing;
-  if (t->stage_used[k]) DL_HIP(hipEventSynchronize(t->stage_ev[k]), "dl_tree_bind(stage slot)");
+  if (t->stage_used[k]) {  // normally long landed: a query, a wait only if it has not
+    hipError_t q = hipEventQuery(t->stage_ev[k]);
+    if (q == hipErrorNotReady)
+      DL_HIP(hipEventSynchronize(t->stage_ev[k]), "dl_tree_bind(stage slot)");
+    else if (q != hipSuccess)
+      return hip_fail(q, "dl_tree_bind(stage slot)");
+  }
   uint64_t* stage = t->h_stage + size_t(k) * size_t(n);
   for (int32_t i = 0; i < n; ++i) stage[i] = ptrs[i];
   uint64_t* segptr = t->d_segptr + size_t(slot) * size_t(n);
