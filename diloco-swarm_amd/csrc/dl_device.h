@@ -105,6 +105,20 @@ __device__ __forceinline__ float4 div4(float4 a, float d) {
   return make_float4(a.x / d, a.y / d, a.z / d, a.w / d);
 }
 
+// The stores of a chunk, one stream at a time: the kUnroll rows of one buffer, then the next
+// buffer's, so each wave writes 4 KiB of one stream back to back. The flat microbenchmark of
+// the 7-stream shape gained 4 % from it (tools/mem_ceiling.hip dps_o); in the product kernels
+// the cold A/B against the row-by-row order is neutral within noise (tools/gpu_ab_cold.sh,
+// profiles/r02_ab_store_order.txt). Rows past the chunk (v >= nv) hold no data and are skipped.
+template <bool NTS>
+__device__ __forceinline__ void store_rows(float* p, const float4 (&x)[kUnroll], int nv, int tid) {
+#pragma unroll
+  for (int u = 0; u < kUnroll; ++u) {
+    const int v = u * kThreads + tid;
+    if (v < nv) stf4<NTS>(p, v, x[u]);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot, int c) {
   return static_cast<T*>(caddr[slot * nchunk + c]);

@@ -123,18 +123,15 @@ struct UnpackSgd {
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        const int v = u * kThreads + tid;
-        if (v < nv) {
-          const float4 gg = DIV ? div4(g[u], d) : g[u];
-          sgd1<MODE>(gg.x, m[u].x, t[u].x, a);
-          sgd1<MODE>(gg.y, m[u].y, t[u].y, a);
-          sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
-          sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
-          stf4<NTS>(th, v, t[u]);
-          if (MODE != 0) stf4<NTS>(mb, v, m[u]);
-          if (in) stf4<NTS>(in, v, t[u]);
-        }
+        const float4 gg = DIV ? div4(g[u], d) : g[u];
+        sgd1<MODE>(gg.x, m[u].x, t[u].x, a);
+        sgd1<MODE>(gg.y, m[u].y, t[u].y, a);
+        sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
+        sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
       }
+      store_rows<NTS>(th, t, nv, tid);
+      if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
+      if (in) store_rows<NTS>(in, t, nv, tid);
       const int i = (nv << 2) + tid;
       if (i < ck.len) {
         float gg = WireIO<W>::ld1(w, i);
@@ -187,18 +184,15 @@ struct DeltaSgd {
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        const int v = u * kThreads + tid;
-        if (v < nv) {
-          const float4 g = sub4(t[u], x[u]);
-          sgd1<MODE>(g.x, m[u].x, t[u].x, a);
-          sgd1<MODE>(g.y, m[u].y, t[u].y, a);
-          sgd1<MODE>(g.z, m[u].z, t[u].z, a);
-          sgd1<MODE>(g.w, m[u].w, t[u].w, a);
-          stf4<NTS>(th, v, t[u]);
-          if (MODE != 0) stf4<NTS>(mb, v, m[u]);
-          stf4<NTS>(in, v, t[u]);
-        }
+        const float4 g = sub4(t[u], x[u]);
+        sgd1<MODE>(g.x, m[u].x, t[u].x, a);
+        sgd1<MODE>(g.y, m[u].y, t[u].y, a);
+        sgd1<MODE>(g.z, m[u].z, t[u].z, a);
+        sgd1<MODE>(g.w, m[u].w, t[u].w, a);
       }
+      store_rows<NTS>(th, t, nv, tid);
+      if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
+      store_rows<NTS>(in, t, nv, tid);
       const int i = (nv << 2) + tid;
       if (i < ck.len) {
         const float g = th[i] - in[i];
@@ -258,20 +252,22 @@ struct DeltaPackSgd {
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        const int v = u * kThreads + tid;
-        if (v < nv) {
-          float4 g = sub4(t[u], x[u]);
-          WireIO<W>::template st4<NTS>(w, v, g);
-          g = make_float4(on_wire(g.x), on_wire(g.y), on_wire(g.z), on_wire(g.w));
-          sgd1<MODE>(g.x, m[u].x, t[u].x, a);
-          sgd1<MODE>(g.y, m[u].y, t[u].y, a);
-          sgd1<MODE>(g.z, m[u].z, t[u].z, a);
-          sgd1<MODE>(g.w, m[u].w, t[u].w, a);
-          stf4<NTS>(th, v, t[u]);
-          if (MODE != 0) stf4<NTS>(mb, v, m[u]);
-          stf4<NTS>(in, v, t[u]);
-        }
+        x[u] = sub4(t[u], x[u]);  // the pseudo-gradient, kept for the wire stores
+        const float4 g = make_float4(on_wire(x[u].x), on_wire(x[u].y), on_wire(x[u].z),
+                                     on_wire(x[u].w));
+        sgd1<MODE>(g.x, m[u].x, t[u].x, a);
+        sgd1<MODE>(g.y, m[u].y, t[u].y, a);
+        sgd1<MODE>(g.z, m[u].z, t[u].z, a);
+        sgd1<MODE>(g.w, m[u].w, t[u].w, a);
       }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int v = u * kThreads + tid;
+        if (v < nv) WireIO<W>::template st4<NTS>(w, v, x[u]);
+      }
+      store_rows<NTS>(th, t, nv, tid);
+      if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
+      store_rows<NTS>(in, t, nv, tid);
       const int i = (nv << 2) + tid;
       if (i < ck.len) {
         const float g0 = th[i] - in[i];

@@ -65,28 +65,34 @@ def main():
     if "flags" in what:
         two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
         one = OuterSync(params, world_size=1, fuse_single=True)
-        two.step()
-        one.step()  # steady-state SGD mode from here on
+        kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True)
+        for e in (two, one, kept):
+            e.step()  # steady-state SGD mode from here on
         kern = {"delta_pack": (two, two.pseudo_gradient, 12),
                 "unpack_sgd": (two, two.apply, 24),
-                "delta_sgd": (one, one.step, 24)}
-        flag_names = {1: "nt_loads", 3: "nt_loads+stores", 0: "plain", 2: "nt_stores"}
+                "delta_sgd": (one, lambda: one._step(None), 24),
+                "delta_pack_sgd": (kept, lambda: kept._step(None), 28)}
+        half = (two.tree.n_chunks + 1) // 2
+        # (flags, grid): grid half = two chunks per workgroup (grid-stride walk)
+        flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (0, 0): "plain",
+                      (2, 0): "nt_stores", (1, half): "nt_loads,2chunks/wg",
+                      (3, half): "nt_loads+stores,2chunks/wg"}
         res = {(k, f): [] for k in kern for f in flag_names}
         for _ in range(a.rounds):
             for (k, f) in res:
                 eng, fn, _ = kern[k]
-                eng.tree.tune(0, f)
+                eng.tree.tune(f[1], f[0])
                 res[(k, f)].append(timed_cold(fn, scrub))
-        two.tree.tune(0, _lib.TUNE_AUTO)
-        one.tree.tune(0, _lib.TUNE_AUTO)
+        for e in (two, one, kept):
+            e.tree.tune(0, _lib.TUNE_AUTO)
         out["flags"] = {}
         for (k, f), ms in res.items():
             s = summarize(ms, kern[k][2] * P)
             out["flags"].setdefault(k, {})[flag_names[f]] = s
-            print(f"{k:11s} {flag_names[f]:16s} med {s['med_ms']:.4f} ms {s['med_GBs']:7.1f} GB/s"
+            print(f"{k:14s} {flag_names[f]:26s} med {s['med_ms']:.4f} ms {s['med_GBs']:7.1f} GB/s"
                   f"  best {s['best_GBs']:7.1f}", flush=True)
-        two.close()
-        one.close()
+        for e in (two, one, kept):
+            e.close()
     if "tiles" in what:
         engs = {}
         for tile in (0, 1024, 2048, 4096, 8192, 16384):

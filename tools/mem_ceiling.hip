@@ -272,6 +272,53 @@ __global__ void __launch_bounds__(T) dps(const Chunk* __restrict__ ch, void* con
   }
 }
 
+// dps with the stores grouped by stream (all wire stores, then θ, then m, then in) instead of
+// by float4 row; BYSTREAM=false is dps<true>'s order
+template <bool BYSTREAM, bool NTW>
+__global__ void __launch_bounds__(T) dps_o(const Chunk* __restrict__ ch, void* const* __restrict__ ca,
+                                           float* th, float* mb, float* w) {
+  const Chunk ck = ch[blockIdx.x];
+  float* in = (float*)ca[blockIdx.x];
+  float* tp = th + ck.poff;
+  float* mp = mb + ck.poff;
+  float* wp = w + ck.poff;
+  f4 x[4], t[4], m[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int v = u * T + threadIdx.x;
+    t[u] = ld(tp, v);
+    x[u] = ld(in, v);
+    m[u] = ld(mp, v);
+  }
+  if constexpr (BYSTREAM) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f4 g = t[u] - x[u];
+      x[u] = g;
+      sgd4(g, m[u], t[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st<NTW>(wp, u * T + threadIdx.x, x[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st(tp, u * T + threadIdx.x, t[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st(mp, u * T + threadIdx.x, m[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st(in, u * T + threadIdx.x, t[u]);
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int v = u * T + threadIdx.x;
+      const f4 g = t[u] - x[u];
+      st<NTW>(wp, v, g);
+      sgd4(g, m[u], t[u]);
+      st(tp, v, t[u]);
+      st(mp, v, m[u]);
+      st(in, v, t[u]);
+    }
+  }
+}
+
 template <bool NTS>
 __global__ void __launch_bounds__(T) rmw3_w(const Chunk* __restrict__ ch, void* const* __restrict__ ca,
                                             float* th, float* mb) {
@@ -396,6 +443,9 @@ int main(int argc, char** argv) {
   ADD("pack_x    XCD-remapped chunks", 12 * nw, hipLaunchKernelGGL(pack_x, dim3(nch), dim3(T), 0, 0, dch, dca, nch, a, c));
   ADD("dps       flat (28 B)        ", 28 * nw, hipLaunchKernelGGL(dps<false>, dim3(nch), dim3(T), 0, 0, dch, dca, inb, b, d, c));
   ADD("dps       walker (28 B)      ", 28 * nw, hipLaunchKernelGGL(dps<true>, dim3(nch), dim3(T), 0, 0, dch, dca, inb, b, d, c));
+  ADD("dps_o     rows, NT wire      ", 28 * nw, hipLaunchKernelGGL((dps_o<false, true>), dim3(nch), dim3(T), 0, 0, dch, dca, b, d, c));
+  ADD("dps_o     by stream, NT wire ", 28 * nw, hipLaunchKernelGGL((dps_o<true, true>), dim3(nch), dim3(T), 0, 0, dch, dca, b, d, c));
+  ADD("dps_o     by stream, plain w ", 28 * nw, hipLaunchKernelGGL((dps_o<true, false>), dim3(nch), dim3(T), 0, 0, dch, dca, b, d, c));
   for (int r = 0; r < rounds; ++r) {
     for (auto& v : vs) {
       hipLaunchKernelGGL(flush_k, dim3(unsigned(nf / 4 / (4 * T))), dim3(T), 0, 0, flush, nf / 4);
