@@ -152,16 +152,18 @@ class Scrubber:
 
 
 def copy_ceiling(dev, mib=1024, reps=10):
-    """What a two-stream kernel of the walker's access shape (dl_copy) moves on this box in
-    this run: read + written bytes / time over `reps` back-to-back copies of `mib` MiB (far
-    beyond the Infinity Cache), default and non-temporal policy. The roofline fractions are
-    read against it beside the 8 TB/s spec peak (boxes differ by ~15 %)."""
+    """What a two-stream copy kernel (dl_copy) moves on this box in this run: read + written
+    bytes / time over `reps` back-to-back copies of `mib` MiB (far beyond the Infinity Cache),
+    default and non-temporal policy, 4 (the walker's shape) and 8 float4 loads in flight per
+    lane; the fastest is the ceiling the roofline fractions are read against beside the 8 TB/s
+    spec peak (boxes differ by ~15 %)."""
     n = (mib << 20) // 4
     a = torch.ones(n, device=dev)
     b = torch.empty(n, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     out = {"bytes_per_copy": 2 * 4 * n}
-    for name, flags in (("plain", 0), ("nt", _lib.TUNE_NT_LOADS)):
+    nt, wide = _lib.TUNE_NT_LOADS, _lib.COPY_WIDE
+    for name, flags in (("plain", 0), ("nt", nt), ("plain_x8", wide), ("nt_x8", nt | wide)):
         _lib.call("dl_copy", a.data_ptr(), b.data_ptr(), 4 * n, flags, st)  # warm the launch
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -172,7 +174,7 @@ def copy_ceiling(dev, mib=1024, reps=10):
         e1.synchronize()
         ms = e0.elapsed_time(e1) / reps
         out[f"{name}_GBs"] = round(2 * 4 * n / (ms * 1e-3) / 1e9, 1)
-    out["GBs"] = max(out["plain_GBs"], out["nt_GBs"])
+    out["GBs"] = max(v for k, v in out.items() if k.endswith("_GBs"))
     del a, b
     torch.cuda.empty_cache()
     return out

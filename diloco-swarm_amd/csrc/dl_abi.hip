@@ -582,9 +582,10 @@ DL_API int dl_copy(const void* src, void* dst, int64_t bytes, int32_t flags, dl_
   if (bytes == 0) return DL_OK;
   DL_TRY(check_packed(src, "dl_copy", "src"));
   DL_TRY(check_packed(dst, "dl_copy", "dst"));
-  if (flags & ~DL_TUNE_NT_LOADS) return fail(DL_E_ARG, "dl_copy: flags 0x%x", flags);
+  if (flags & ~(DL_TUNE_NT_LOADS | DL_COPY_WIDE))
+    return fail(DL_E_ARG, "dl_copy: flags 0x%x", flags);
   hipError_t e = dl::launch_copy(src, dst, bytes / 16, (flags & DL_TUNE_NT_LOADS) != 0,
-                                 static_cast<hipStream_t>(s));
+                                 (flags & DL_COPY_WIDE) != 0, static_cast<hipStream_t>(s));
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_copy");
 }
 

@@ -84,7 +84,9 @@ hipError_t launch_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stre
 // dl_tree_bind: out[c] = segptr[chunks[c].seg] + 4 * loff[c] for every chunk c
 hipError_t launch_resolve_chunks(const Chunk* chunks, const int64_t* loff, const uint64_t* segptr,
                                  int32_t nch, void** out, hipStream_t s);
-// flat 16-B streaming copy (the same-run copy ceiling of bench.py): n16 float4, nt = NT policy
-hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, hipStream_t s);
+// flat 16-B streaming copy (the same-run copy ceiling of bench.py): n16 float4, nt = NT
+// policy, wide = 8 instead of 4 float4 loads in flight per lane
+hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, bool wide,
+                       hipStream_t s);
 
 }  // namespace dl

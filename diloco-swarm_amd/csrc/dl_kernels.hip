@@ -427,24 +427,24 @@ __global__ void __launch_bounds__(kThreads)
     out[c] = segptr[chunks[c].seg] + uint64_t(loff[c]) * sizeof(float);
 }
 
-// Calibration copy: the walker's access shape (one workgroup per 16 KiB, every 16-B load of
-// the workgroup issued before its stores) on one flat buffer -- what the memory system gives
-// a two-stream kernel on this box in this run (bench.py's copy ceiling).
-template <bool NT>
+// Calibration copy (bench.py's same-run copy ceiling): U float4 loads per lane issued before
+// the stores, one workgroup per U*1024 float4. U = 4 is the walker's access shape; U = 8 (twice
+// the bytes in flight) is the fastest flat copy measured (tools/mem_ceiling.hip copy<8>).
+template <bool NT, int U>
 __global__ void __launch_bounds__(kThreads)
     k_copy(const float* __restrict__ src, float* __restrict__ dst, int64_t n16) {
-  const int64_t base = int64_t(blockIdx.x) * (kThreads * kUnroll);
-  float4 x[kUnroll];
+  const int64_t base = int64_t(blockIdx.x) * (kThreads * U);
+  float4 x[U];
   const float* s = src + base * 4;
   float* d = dst + base * 4;
   const int64_t rem = n16 - base;
 #pragma unroll
-  for (int u = 0; u < kUnroll; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int v = u * kThreads + int(threadIdx.x);
     if (v < rem) x[u] = ldf4<NT>(s, v);
   }
 #pragma unroll
-  for (int u = 0; u < kUnroll; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int v = u * kThreads + int(threadIdx.x);
     if (v < rem) stf4<NT>(d, v, x[u]);
   }
@@ -463,18 +463,21 @@ hipError_t launch_resolve_chunks(const Chunk* chunks, const int64_t* loff, const
   return hipGetLastError();
 }
 
-hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, hipStream_t s) {
-  if (n16 <= 0) return hipSuccess;
-  const int64_t per = kThreads * kUnroll;
+template <bool NT, int U>
+static hipError_t copy_u(const void* src, void* dst, int64_t n16, hipStream_t s) {
+  const int64_t per = kThreads * U;
   const int64_t grid = (n16 + per - 1) / per;
   if (grid > INT32_MAX) return hipErrorInvalidValue;
-  if (nt)
-    hipLaunchKernelGGL(k_copy<true>, dim3(uint32_t(grid)), dim3(kThreads), 0, s,
-                       static_cast<const float*>(src), static_cast<float*>(dst), n16);
-  else
-    hipLaunchKernelGGL(k_copy<false>, dim3(uint32_t(grid)), dim3(kThreads), 0, s,
-                       static_cast<const float*>(src), static_cast<float*>(dst), n16);
+  hipLaunchKernelGGL((k_copy<NT, U>), dim3(uint32_t(grid)), dim3(kThreads), 0, s,
+                     static_cast<const float*>(src), static_cast<float*>(dst), n16);
   return hipGetLastError();
+}
+
+hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, bool wide,
+                       hipStream_t s) {
+  if (n16 <= 0) return hipSuccess;
+  if (wide) return nt ? copy_u<true, 8>(src, dst, n16, s) : copy_u<false, 8>(src, dst, n16, s);
+  return nt ? copy_u<true, 4>(src, dst, n16, s) : copy_u<false, 4>(src, dst, n16, s);
 }
 
 hipError_t launch_delta_pack(const Launch& L, int inner_slot, const float* outer, void* wire,

@@ -302,9 +302,11 @@ DL_API int dl_xgmi_delta_sgd(const uint64_t* inners, const uint64_t* thetas, int
 
 /* ---- calibration ------------------------------------------------------------------------
  * dst[0:bytes) = src[0:bytes) with the segment walker's access shape (one 256-lane
- * workgroup per 16 KiB, 4 float4 loads per lane before the stores); flags DL_TUNE_NT_LOADS =
- * non-temporal loads and stores. bench.py times it in the same run as the outer step: the
- * copy ceiling its roofline fractions are read against (not on the reference's path). */
+ * workgroup per 16 KiB, 4 float4 loads per lane before the stores); flags: DL_TUNE_NT_LOADS =
+ * non-temporal loads and stores, DL_COPY_WIDE = 8 float4 loads per lane (32 KiB per
+ * workgroup). bench.py times every variant in the same run as the outer step and reads its
+ * roofline fractions against the fastest: the copy ceiling (not on the reference's path). */
+#define DL_COPY_WIDE 8
 DL_API int dl_copy(const void* src, void* dst, int64_t bytes, int32_t flags, dl_stream_t stream);
 
 DL_API const char* dl_last_error(void);

@@ -164,3 +164,19 @@ def test_dropin_sequence_under_concurrent_default_stream_traffic(placement, writ
         assert rec[f"theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
         assert rec[f"buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes()
         assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+
+
+@pytest.mark.parametrize("flags", [0, 1, 8, 9])
+def test_copy_kernel_copies_exactly(flags):
+    """dl_copy (the bench's copy-ceiling kernel and its cache scrub) in every variant: exact
+    bytes, partial last workgroup, nothing written past the end."""
+    for n16 in (1, 1023, 1024, 2049, 1 << 18):
+        src = torch.arange(4 * n16, dtype=torch.float32, device=DEV)
+        dst = torch.full((4 * n16 + 64,), -1.0, device=DEV)
+        _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 16 * n16, flags,
+                  torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(dst[:4 * n16], src), (flags, n16)
+        assert bool((dst[4 * n16:] == -1.0).all()), (flags, n16)
+    with pytest.raises(_lib.DilocoHipError, match="multiple of 16"):
+        _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 20, flags, None)
