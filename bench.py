@@ -1340,6 +1340,9 @@ def main():
                         "frac_of_rccl_allreduce": round(bw / arbw, 4),
                         "frac_of_link_peak": round(bw / ((ws - 1) * XGMI_LINK_GBS), 4),
                     }
+            if ws == 1:  # the headline's one-pass step on the 1.3B tree
+                leg(f"{es.name}_fused_keep_wire", run_tree, es, dev, ws, rank, ks, 1, wire, cap,
+                    True, False, None, "rccl", None, False, True)
             if wire == torch.float32:  # BASELINE config #5: bf16 wire + SGD fused into unpack
                 leg(f"{es.name}_bf16_wire", run_tree, es, dev, ws, rank, ks, 1, torch.bfloat16,
                     cap)
