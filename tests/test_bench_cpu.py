@@ -50,3 +50,29 @@ def test_finished_run_prints_one_line():
 def test_watchdog_before_headline_fails_the_run():
     rc, lines, _ = _run(1.0, False, False)
     assert rc != 0 and lines == []
+
+
+def test_cpu_baseline_with_two_gloo_processes():
+    """The N > 1 CPU baseline (bench.cpu_baseline_dist): two CPU processes under gloo (GPUs
+    hidden, as bench's child legs run it) step the reference's per-tensor sequence with its
+    per-tensor all_reduce on the tiny tree; rank 0 writes one record with cores = 2."""
+    import socket
+    import tempfile
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = os.path.join(tempfile.mkdtemp(prefix="dl_cpub_"), "cb.json")
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), os.path.join(REPO, "bench.py"), "--gpus", "2", "--tree",
+                        "tiny", "--child-legs", "cpu_baseline", "--child-out", out,
+                        "--deadline", "100"], capture_output=True, text=True, timeout=170,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    with open(out) as f:
+        r = json.load(f)
+    assert r["cores"] == 2 and r["kind"] == "port" and r["value"] > 0
+    assert "2 CPU processes" in r["sample"]
