@@ -229,6 +229,7 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
     torch.cuda.synchronize()
     first = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
     second = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+    warm_span = sum(e[0].elapsed_time(e[2]) for e in ev) / steps
     pmc = load_pmc(spec.name) if wire == torch.float32 else {}
     res = {"tree": spec.name, "params": P, "tensors": len(spec.params()),
            "padded": eng.tree.total, "buckets": eng.tree.n_buckets, "chunks": eng.tree.n_chunks,
@@ -283,8 +284,13 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         c_second = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
         c_step = sum(e[0].elapsed_time(e[2]) for e in ev) / steps
         res["cold"] = {"step_ms": round(c_step, 5), "value": 4.0 * P / (c_step * 1e-3) / 1e9,
+                       # the same event span in the warm instrumented pass: the like-for-like
+                       # comparison (the headline value is wall-clock, gaps between steps in)
+                       "warm_step_ms": round(warm_span, 5),
+                       "warm_value": 4.0 * P / (warm_span * 1e-3) / 1e9,
                        "note": "Infinity Cache scrubbed before each step (512 MiB copy, "
-                               "outside the events); step = the kernels' event span"}
+                               "outside the events); step = the kernels' event span, no "
+                               "inter-step gap (compare warm_step_ms, not the headline)"}
         if fuse:
             res["cold"]["kernels"] = {fused_name: kernel_entry(fused_bytes, c_first)}
         elif tiled:
@@ -1245,7 +1251,7 @@ def main():
         ks = cold["kernels"]
         dom = max(ks, key=lambda k: ks[k]["avg_ms"])
         roof_cold = dict(with_copy_ceiling(ks[dom], cgbs), kernel=dom)
-        cold = dict(cold, value=round(cold["value"], 3),
+        cold = dict(cold, value=round(cold["value"], 3), warm_value=round(cold["warm_value"], 3),
                     kernels={k: with_copy_ceiling(v, cgbs) for k, v in ks.items()})
     em.line = {
         "metric": METRIC,
