@@ -93,6 +93,39 @@ def main():
                   f"  best {s['best_GBs']:7.1f}", flush=True)
         for e in (two, one, kept):
             e.close()
+    if "q8" in what:  # the int8 wire's kernels, one bucket (every launch covers the tree)
+        from diloco_amd.kernels import Q8_SLOT
+
+        e = OuterSync(params, world_size=1, wire_dtype=torch.int8, bucket_cap_elems=0)
+        e.step()
+        nch, m, _ = e.q8_plan[0]
+        region = e.q8_region(0)
+        slot_bytes = nch * Q8_SLOT
+        half = (e.tree.n_chunks + 1) // 2
+
+        def red():
+            e.k.q8_reduce(region, 1, m, 1, region)
+
+        def unpack():
+            e.apply(0)
+
+        kern = {"delta_q8": (lambda: e.pseudo_gradient(0), 8 * P + slot_bytes),
+                "q8_reduce": (red, 2 * slot_bytes),
+                "unpack_sgd_q8": (unpack, slot_bytes + 20 * P)}
+        shapes = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (1, half): "nt_loads,2chunks/wg"}
+        res = {(k, f): [] for k in kern for f in shapes}
+        for _ in range(a.rounds):
+            for (k, f) in res:
+                e.tree.tune(f[1], f[0])
+                res[(k, f)].append(timed_cold(kern[k][0], scrub))
+        e.tree.tune(0, _lib.TUNE_AUTO)
+        out["q8"] = {}
+        for (k, f), ms in res.items():
+            s = summarize(ms, kern[k][1])
+            out["q8"].setdefault(k, {})[shapes[f]] = s
+            print(f"{k:14s} {shapes[f]:26s} med {s['med_ms']:.4f} ms {s['med_GBs']:7.1f} GB/s"
+                  f"  best {s['best_GBs']:7.1f}", flush=True)
+        e.close()
     if "tiles" in what:
         engs = {}
         for tile in (0, 1024, 2048, 4096, 8192, 16384):
