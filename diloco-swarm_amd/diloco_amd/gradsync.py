@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .kernels import default_kernels
-from .outer import pipelined_buckets
+from .outer import _Done, pipelined_buckets
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_GRAD
 
 
@@ -45,6 +45,9 @@ class GradSync:
             self._sync()
             return
         cur = torch.cuda.current_stream(self.device)
+        if cur == self.stream:
+            self._sync()
+            return
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             self._sync()
@@ -62,11 +65,14 @@ class GradSync:
             lo, hi = self.tree.bucket_ranges[b]
             return self.wire[lo:hi]
 
+        # one replica with no process group: the all-reduce is the identity (the rebinding,
+        # gather and /1 still run, so the path is exercised on a one-GPU machine)
+        local = self.world_size == 1 and not dist.is_initialized()
         pipelined_buckets(
             self.tree.n_buckets,
             lambda b: self.k.gather(self.tree, b, SLOT_GRAD, self.wire),
-            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=self.group,
-                                      async_op=True),
+            lambda b: _Done() if local else dist.all_reduce(
+                view(b), op=dist.ReduceOp.SUM, group=self.group, async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, self.wire, self.world_size, SLOT_GRAD),
         )
 

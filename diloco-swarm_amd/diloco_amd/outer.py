@@ -91,7 +91,7 @@ class OuterSync:
         bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS,
         kernels=None,
         fuse_single: bool = True,
-        side_stream: bool = True,
+        side_stream: Optional[bool] = None,
         shard: Optional[bool] = None,
         rank: Optional[int] = None,
         exchange: str = "rccl",
@@ -214,6 +214,14 @@ class OuterSync:
         # back into it: work other threads put on the default stream meanwhile (the
         # reference's p2p send threads copy activations with .to("cpu"), src/comm.py:38)
         # overlaps the outer step instead of queueing behind it.
+        # side_stream=None (auto): a side stream wherever the step has stages to order against
+        # the collectives; the one-replica fused step is ONE kernel, so it launches on the
+        # caller's stream -- the two joins would add two cross-queue hops (22 us of a 0.61 ms
+        # step, profiles/r02_stream_ab.json) and the join back orders the caller behind the
+        # kernel anyway.
+        if side_stream is None:
+            side_stream = not (self.world_size == 1 and self.fuse_single and not self.q8
+                               and not self.xgmi and not self.sharded)
         self.stream = (torch.cuda.Stream(self.device)
                        if side_stream and self.device.type == "cuda" else None)
 
@@ -387,6 +395,9 @@ class OuterSync:
             self._step(pipeline)
             return
         cur = torch.cuda.current_stream(self.device)
+        if cur == self.stream:  # the caller already runs on the engine's stream
+            self._step(pipeline)
+            return
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             self._step(pipeline)

@@ -119,15 +119,19 @@ class _DefaultStreamTraffic:
         return False
 
 
-@pytest.mark.parametrize("fuse", [True, False])
-def test_outer_step_under_concurrent_default_stream_traffic(fuse):
+@pytest.mark.parametrize("fuse,side_stream", [(True, None), (True, True), (False, None),
+                                              (False, False)])
+def test_outer_step_under_concurrent_default_stream_traffic(fuse, side_stream):
     from diloco_amd.outer import OuterSync
 
     spec = get_tree("micro")
     g = load_npz("micro_n1.npz")
     shapes = [s for _, s in spec.params()]
     params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
-    e = OuterSync(params, world_size=1, fuse_single=fuse)
+    e = OuterSync(params, world_size=1, fuse_single=fuse, side_stream=side_stream)
+    # auto policy: the one-kernel fused step on the caller's stream, the two-kernel step on
+    # the engine's side stream
+    assert (e.stream is None) == (side_stream is False or (side_stream is None and fuse))
     with _DefaultStreamTraffic() as traffic:
         for s in (1, 2):
             th = [t.reshape(-1) for t in e.unpacked(e.theta)]
