@@ -608,20 +608,20 @@ def run_q8(spec, dev, ws, rank, steps, warmup, cap):
            "value_aggregate": ws * 4.0 * P / (dt / steps) / 1e9,
            "wire": "int8", "wire_bytes_per_param": round(slot_bytes / P, 4),
            "bus_bytes_per_step": 2.0 * (ws - 1) / ws * slot_bytes}
-    if ws == 1:  # the three kernels, each over the whole tree, timed in place
+    if ws == 1:  # the three kernels, each over the whole tree (as the one-replica step runs
+        # them: no bucket is padded at n = 1), timed in place
+        from diloco_amd.plan import SLOT_INNER
+
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         tot = [0.0, 0.0, 0.0]
         for _ in range(steps):
             ev[0].record()
-            for b in range(nb):
-                eng.pseudo_gradient(b)
+            eng.k.delta_q8(eng.tree, -1, SLOT_INNER, eng.theta, eng.q_slots)
             ev[1].record()
-            for b in range(nb):
-                region = eng.q8_region(b)
-                eng.k.q8_reduce(region, 1, eng.q8_plan[b][1], 1, region)
+            eng.k.q8_reduce(eng.q_slots, 1, eng.tree.n_chunks, 1, eng.q_slots)
             ev[2].record()
-            for b in range(nb):
-                eng.apply(b)
+            eng.k.unpack_sgd_q8(eng.tree, -1, eng.q_slots, eng.theta, eng.mom, eng.lr,
+                                eng.momentum, eng.nesterov, False, SLOT_INNER)
             ev[3].record()
             eng.steps_done += 1
             torch.cuda.synchronize()

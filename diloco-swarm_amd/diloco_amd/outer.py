@@ -210,6 +210,7 @@ class OuterSync:
             if not self.peers.ok:
                 raise RuntimeError(f"exchange='xgmi' unavailable: {self.peers.reason}")
         self.steps_done = 0
+        self._step_bound = False
         # step() runs on its own stream, ordered after the caller's current stream and joined
         # back into it: work other threads put on the default stream meanwhile (the
         # reference's p2p send threads copy activations with .to("cpu"), src/comm.py:38)
@@ -242,12 +243,20 @@ class OuterSync:
         self._arena_ptrs = [o.data_ptr() for o in self._objs]
         self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
 
+    def _bind_inner(self) -> None:
+        """Point the tree's inner slot at the inner params' current storage (a no-op when
+        unchanged). step() binds once up front; the per-bucket building blocks bind when they
+        are called on their own (checking 292 addresses per bucket would cost ~1 ms of host
+        time per T1.3B step)."""
+        if not self._step_bound:
+            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+
     def pseudo_gradient(self, bucket: int = ALL) -> None:
         """wire[bucket] = θ_outer - inner (a2); int8 wire: its quantised slots."""
         if self.xgmi_inner:
             raise RuntimeError("exchange='xgmi_inner' has no wire: the exchange kernel forms "
                                "the pseudo-gradient; use step()")
-        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+        self._bind_inner()
         if self.q8:
             self.k.delta_q8(self.tree, bucket, SLOT_INNER, self.theta, self.q8_region(bucket))
         else:
@@ -327,7 +336,7 @@ class OuterSync:
 
     def write_inner(self, bucket: int) -> None:
         """a5: inner = θ_outer for one bucket (dl_scatter)."""
-        self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+        self._bind_inner()
         self.k.scatter(self.tree, bucket, self.theta, SLOT_INNER)
 
     def momentum_full(self) -> Optional[torch.Tensor]:
@@ -406,6 +415,16 @@ class OuterSync:
     def _step(self, pipeline: Optional[bool]) -> None:
         if pipeline is None:
             pipeline = self.world_size > 1
+        if not self.xgmi_inner:
+            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
+        self._step_bound = True
+        try:
+            self._step_body(pipeline)
+        finally:
+            self._step_bound = False
+        self.steps_done += 1
+
+    def _step_body(self, pipeline: bool) -> None:
         if self.q8:
             self._step_q8(pipeline)
         elif self.xgmi:
@@ -417,22 +436,18 @@ class OuterSync:
                               lambda b: self.all_reduce(b, async_op=True), self.apply)
         elif self.fuse_single and self.keep_wire:
             # src/comm.py:118-119: one peer -> no all-reduce and no division
-            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.delta_pack_sgd(self.tree, ALL, SLOT_INNER, self.theta, self.wire, self.mom,
                                   self.lr, self.momentum, self.nesterov, self.steps_done == 0)
         elif self.fuse_single:
-            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.delta_sgd(self.tree, ALL, SLOT_INNER, self.theta, self.mom, self.lr,
                              self.momentum, self.nesterov, self.steps_done == 0)
         elif self.tile_chunks:
-            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.pack_sgd_tiled(self.tree, ALL, SLOT_INNER, self.theta, self.wire, self.mom,
                                   self.lr, self.momentum, self.nesterov, self.steps_done == 0,
                                   self.tile_chunks)
         else:
             self.pseudo_gradient(ALL)
             self.apply(ALL)
-        self.steps_done += 1
 
     def _step_sharded(self) -> None:
         """pack(b) -> RS(b) | shard SGD(b) -> AG(b) | scatter(b), overlapped across buckets:
@@ -486,12 +501,20 @@ class OuterSync:
         if self.xgmi_inner:  # inner = θ: one flat copy of the arena (padding stays zero)
             self.inner_arena.copy_(self.theta)
         else:
-            self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.scatter(self.tree, ALL, self.theta, SLOT_INNER)
 
     def _step_q8(self, pipeline: bool) -> None:
         nb = self.tree.n_buckets
-        if not pipeline:  # one replica: the average of one is its own re-quantised slots
+        if not pipeline and self.world_size == 1:
+            # one replica: the average of one is its own re-quantised slots. At n = 1 no bucket
+            # is padded, so the buckets' slots are the tree's chunks in order and each kernel
+            # covers the whole tree in one launch
+            self.k.delta_q8(self.tree, ALL, SLOT_INNER, self.theta, self.q_slots)
+            self.k.q8_reduce(self.q_slots, 1, self.tree.n_chunks, 1, self.q_slots)
+            self.k.unpack_sgd_q8(self.tree, ALL, self.q_slots, self.theta, self.mom, self.lr,
+                                 self.momentum, self.nesterov, self.steps_done == 0, SLOT_INNER)
+            return
+        if not pipeline:  # no exchange requested: each replica re-quantises its own slots
             for b in range(nb):
                 self.pseudo_gradient(b)
                 nch, m, _ = self.q8_plan[b]
