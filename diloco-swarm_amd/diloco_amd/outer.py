@@ -549,6 +549,8 @@ class OuterSync:
         if len(th) != len(self.params) or any(a.numel() != p.numel()
                                                for a, p in zip(th, self.params)):
             raise ValueError("state_dict does not match this engine's parameter tree")
+        if int(state["steps"]) > 0 and self.momentum != 0 and state.get("momentum") is None:
+            raise ValueError("state_dict after step >= 1 must carry the momentum")
         with torch.no_grad():
             for dst, src in zip(self.unpacked(self.theta), th):
                 dst.copy_(src.view(dst.shape))
@@ -571,8 +573,6 @@ class OuterSync:
                 for b in range(self.tree.n_buckets):
                     self.th_shard_view(b).copy_(self.theta_shard_of(b))
         self.steps_done = int(state["steps"])
-        if self.steps_done > 0 and self.momentum != 0 and state.get("momentum") is None:
-            raise ValueError("state_dict after step >= 1 must carry the momentum")
         if write_inner:
             self.k.bind(self.tree, SLOT_INNER, self.params, self.device)
             self.k.scatter(self.tree, ALL, self.theta, SLOT_INNER)
