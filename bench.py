@@ -628,10 +628,11 @@ def run_q8(spec, dev, ws, rank, steps, warmup, cap):
             for i in range(3):
                 tot[i] += ev[i].elapsed_time(ev[i + 1])
         ms = [t / steps for t in tot]
+        pmc = load_pmc(spec.name)  # the same whole-tree launches (tools/kernel_driver.py)
         res["kernels"] = {
-            "delta_q8": kernel_entry(8 * P + slot_bytes, ms[0]),
-            "q8_reduce": kernel_entry(2 * slot_bytes, ms[1]),
-            "unpack_sgd_q8": kernel_entry(slot_bytes + 20 * P, ms[2]),
+            "delta_q8": kernel_entry(8 * P + slot_bytes, ms[0], pmc.get("delta_q8")),
+            "q8_reduce": kernel_entry(2 * slot_bytes, ms[1], pmc.get("q8_reduce")),
+            "unpack_sgd_q8": kernel_entry(slot_bytes + 20 * P, ms[2], pmc.get("unpack_sgd_q8")),
         }
     eng.close()
     del eng
