@@ -326,6 +326,8 @@ namespace {
 constexpr int32_t kAutoDelta = DL_TUNE_NT_LOADS;
 constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 constexpr int32_t kAutoOther = DL_TUNE_NT_LOADS;
+// int8 encoder: its one 16-B payload store per lane non-temporal (tools/q8_layout.hip)
+constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 
 int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who,
                 int32_t auto_flags = kAutoOther) {
@@ -658,7 +660,7 @@ DL_API int dl_xgmi_delta_sgd(const uint64_t* inners, const uint64_t* thetas, int
 DL_API int dl_delta_q8(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,
                        void* slots, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_delta_q8", kAutoDelta));
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_q8", kAutoDeltaQ8));
   DL_TRY(check_slot(t, inner_slot, "dl_delta_q8"));
   DL_TRY(check_packed(outer, "dl_delta_q8", "outer"));
   DL_TRY(check_packed(slots, "dl_delta_q8", "slots"));

@@ -52,7 +52,13 @@ __device__ __forceinline__ float amax4(float4 x) {
 typedef DL_GLOBAL uint32_t* gu32;
 typedef DL_GLOBAL const uint32_t* gcu32;
 
-// a2 with the int8 codec: slot(c) <- quantise(θ - inner) over chunk c
+// a2 with the int8 codec: slot(c) <- quantise(θ - inner) over chunk c.
+// The 4096-B payload is assembled in LDS (zero beyond the chunk's length) and leaves in ONE
+// 16-B store per lane: four 4-B-per-lane stores per lane (256 B per wave instruction) cost
+// ~10 % of the kernel cold at T1.3B size against one 1-KB-per-wave store (tools/q8_layout.hip,
+// profiles/r02_q8_layout.txt).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 struct DeltaQ8 {
   int inner_slot;
   const float* outer;
@@ -60,12 +66,15 @@ struct DeltaQ8 {
   int c0;
   template <bool NTL, bool NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    __shared__ u32x4 stage[DL_CHUNK_ELEMS / 16];  // the payload, 16 B per lane
+    uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
+    uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
     const float* in = slot_ptr<const float>(caddr, nchunk, inner_slot, c);
     const float* th = outer + ck.poff;
     uint8_t* slot = slots + size_t(c - c0) * DL_Q8_SLOT_BYTES;
-    uint8_t* q = slot + kQ8Header;
     const int nv = ck.len >> 2;
     const bool vec = aligned16(in);
+    stage[tid] = u32x4{0u, 0u, 0u, 0u};  // bytes past the chunk's length stay zero
     float4 d[kUnroll];
     float dt = 0.f;  // vector path: the < 4 tail elements
     float am = 0.f;
@@ -92,15 +101,15 @@ struct DeltaQ8 {
       }
     }
     am = fmaxf(am, fabsf(dt));
-    const float s = block_amax(am) / 127.f;
+    const float s = block_amax(am) / 127.f;  // its barriers also order the zeroing above
     if (vec) {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) ((gu32)q)[v] = pack4(d[u], s);
+        if (v < nv) st32[v] = pack4(d[u], s);
       }
       const int i = (nv << 2) + tid;
-      if (i < ck.len) q[i] = uint8_t(q8(dt, s));
+      if (i < ck.len) st8[i] = uint8_t(q8(dt, s));
     } else {
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
@@ -108,11 +117,19 @@ struct DeltaQ8 {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = (4 * u + j) * kThreads + tid;
-          if (i < ck.len) q[i] = uint8_t(q8(e[j], s));
+          if (i < ck.len) st8[i] = uint8_t(q8(e[j], s));
         }
       }
     }
+    __syncthreads();
+    const u32x4 w = stage[tid];
+    DL_GLOBAL u32x4* q = (DL_GLOBAL u32x4*)(slot + kQ8Header);
+    if constexpr (NTS)
+      __builtin_nontemporal_store(w, q + tid);
+    else
+      q[tid] = w;
     if (tid == 0) *reinterpret_cast<float*>(slot) = s;
+    __syncthreads();  // `stage` is reused by the workgroup's next chunk
   }
 };
 
@@ -208,9 +225,14 @@ __global__ void __launch_bounds__(kThreads)
     am = fmaxf(am, amax4(acc[u]));
   }
   const float s = block_amax(am) / 127.f;
-  uint8_t* o = out + size_t(j) * DL_Q8_SLOT_BYTES;
+  // the averaged payload leaves as one non-temporal 16-B store per lane (as in DeltaQ8)
+  __shared__ u32x4 stage[DL_CHUNK_ELEMS / 16];
+  uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
 #pragma unroll
-  for (int u = 0; u < kUnroll; ++u) ((gu32)(o + kQ8Header))[u * kThreads + tid] = pack4(acc[u], s);
+  for (int u = 0; u < kUnroll; ++u) st32[u * kThreads + tid] = pack4(acc[u], s);
+  __syncthreads();
+  uint8_t* o = out + size_t(j) * DL_Q8_SLOT_BYTES;
+  __builtin_nontemporal_store(stage[tid], (DL_GLOBAL u32x4*)(o + kQ8Header) + tid);
   if (tid == 0) *reinterpret_cast<float*>(o) = s;
 }
 

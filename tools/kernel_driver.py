@@ -43,6 +43,27 @@ def main():
     for e in (q8, sh, xg):
         for _ in range(reps + 1):
             e.step()
+    # the per-step DP gradient sync at one replica (dl_gather -> identity -> dl_unpack_avg),
+    # one bucket so each launch covers the tree
+    from diloco_amd.gradsync import GradSync
+
+    grads = [torch.nn.Parameter(torch.zeros_like(p)) for p in params]
+    for g in grads:
+        g.grad = torch.randn_like(g)
+    gs = GradSync(grads, None, 1, bucket_cap_elems=0)
+    for _ in range(reps + 1):
+        gs.sync()
+    gs.close()
+    del grads
+    # the pipeline Serializer (src/serializer.py:11-15) framing the reference's message, a
+    # (32, 1024, 768) activation, fp32 and bf16 payloads
+    from diloco_amd.serializer import Serializer
+
+    ser = Serializer((32, 1024, 768))
+    act = torch.randn(32, 1024, 768, device=dev)
+    for x in (act, act.bfloat16()):
+        for _ in range(reps + 1):
+            ser.serialize(x, (3, 7))
     # last: exchange="xgmi_inner" moves `params` into its own arena
     xi = OuterSync(params, world_size=1, exchange="xgmi_inner")
     for e in (xi,):

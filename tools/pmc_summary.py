@@ -21,7 +21,8 @@ def short(name):
              "k_q8_reduce": "q8_reduce", "DeltaPackSgd": "delta_pack_sgd",
              "DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd",
              "UnpackAvg": "unpack_avg", "DeltaSgd": "delta_sgd", "Gather": "gather",
-             "Scatter": "scatter", "k_fill_synth": "fill_synth"}
+             "Scatter": "scatter", "k_fill_synth": "fill_synth",
+             "k_serialize_f32x4": "serialize_f32", "k_serialize<unsigned short>": "serialize_bf16"}
     if "k_xgmi_reduce_sgd" in name and ", true>" in name:
         return "xgmi_delta_sgd"  # the pack-free variant (exchange="xgmi_inner")
     for k, v in names.items():
