@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=11)
     ap.add_argument("--what", default="flags,tiles")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--wire", default="f32", help="flags: the wire of the two-kernel and "
+                    "kept-wire engines (f32 | bf16)")
     a = ap.parse_args()
     from bench import Scrubber
 
@@ -63,15 +65,18 @@ def main():
     out = {"tree": a.tree, "params": P, "rounds": a.rounds}
     what = a.what.split(",")
     if "flags" in what:
-        two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
+        wd = torch.bfloat16 if a.wire == "bf16" else torch.float32
+        wb = 2 if a.wire == "bf16" else 4
+        out["wire"] = a.wire
+        two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0, wire_dtype=wd)
         one = OuterSync(params, world_size=1, fuse_single=True)
-        kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True)
+        kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True, wire_dtype=wd)
         for e in (two, one, kept):
             e.step()  # steady-state SGD mode from here on
-        kern = {"delta_pack": (two, two.pseudo_gradient, 12),
-                "unpack_sgd": (two, two.apply, 24),
+        kern = {"delta_pack": (two, two.pseudo_gradient, 8 + wb),
+                "unpack_sgd": (two, two.apply, 20 + wb),
                 "delta_sgd": (one, lambda: one._step(None), 24),
-                "delta_pack_sgd": (kept, lambda: kept._step(None), 28)}
+                "delta_pack_sgd": (kept, lambda: kept._step(None), 24 + wb)}
         half = (two.tree.n_chunks + 1) // 2
         # (flags, grid): grid half = two chunks per workgroup (grid-stride walk)
         flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (0, 0): "plain",

@@ -10,6 +10,8 @@
 //   q8_split   4096-B payload slots (aligned) + a dense fp32 scale array
 //   q8_noscale q8_4160 without the 4-B scale store (payload only)
 //   q8_nobar   q8_4160 with the amax taken per wave (no workgroup barrier; a per-1024 scale)
+//   q8_lds*    the payload staged in LDS, one 16-B store per lane (plain / non-temporal)
+//   packbf_*   the bf16 wire's delta_pack (10 B/elem): 8-B stores per lane vs LDS-staged 16-B
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -fhip-fp32-correctly-rounded-divide-sqrt tools/q8_layout.hip -o build/q8_layout
 #include <hip/hip_runtime.h>
@@ -136,6 +138,51 @@ __global__ void __launch_bounds__(T) q8lds(const float* th, const float* in, uns
   }
 }
 
+// bf16 wire (dl_delta_pack's bf16 shape, 10 B/elem): 4 bf16 = 8 B per lane per store as the
+// product stores them, or the chunk's 8 KB staged in LDS and written as two 16-B stores per lane
+__device__ __forceinline__ unsigned short bf16_rne(float x) {
+  unsigned u = __float_as_uint(x);
+  return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u2 bf4(f4 x) {
+  return u2{unsigned(bf16_rne(x.x)) | (unsigned(bf16_rne(x.y)) << 16),
+            unsigned(bf16_rne(x.z)) | (unsigned(bf16_rne(x.w)) << 16)};
+}
+template <bool NTS>
+__global__ void __launch_bounds__(T) packbf_8(const float* th, const float* in, unsigned short* w) {
+  const long base = long(blockIdx.x) * (CH / 4);
+  f4 d[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) d[u] = ld(th, base + u * T + threadIdx.x) - ld(in, base + u * T + threadIdx.x);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    G u2* p = (G u2*)w + base + u * T + threadIdx.x;
+    if constexpr (NTS) __builtin_nontemporal_store(bf4(d[u]), p);
+    else *p = bf4(d[u]);
+  }
+}
+template <bool NTS>
+__global__ void __launch_bounds__(T) packbf_lds(const float* th, const float* in, unsigned short* w) {
+  __shared__ u2 stage[CH / 4];
+  const long base = long(blockIdx.x) * (CH / 4);
+  f4 d[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) d[u] = ld(th, base + u * T + threadIdx.x) - ld(in, base + u * T + threadIdx.x);
+#pragma unroll
+  for (int u = 0; u < U; ++u) stage[u * T + threadIdx.x] = bf4(d[u]);
+  __syncthreads();
+  const u4v* s4 = reinterpret_cast<const u4v*>(stage);
+  G u4v* o = (G u4v*)(w + base * 4);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const u4v v = s4[k * T + threadIdx.x];
+    if constexpr (NTS) __builtin_nontemporal_store(v, o + k * T + threadIdx.x);
+    else o[k * T + threadIdx.x] = v;
+  }
+}
+
 __global__ void __launch_bounds__(T) flush_k(float* p, long n4) {
   for (long v = blockIdx.x * long(T) + threadIdx.x; v < n4; v += long(gridDim.x) * T) {
     f4 x = ((G f4*)p)[v];
@@ -194,6 +241,11 @@ int main(int argc, char** argv) {
   ADD("q8_lds_nt  4160, NT 16-B     ", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, true>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_split 4096+scales     ", q8b, hipLaunchKernelGGL((q8lds<4096, 0, true, false>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_split_nt              ", q8b, hipLaunchKernelGGL((q8lds<4096, 0, true, true>), g, b, 0, 0, th, in, slots, scales));
+  unsigned short* wb = reinterpret_cast<unsigned short*>(w);
+  ADD("packbf_8   8-B stores        ", 10.0 * n, hipLaunchKernelGGL(packbf_8<false>, g, b, 0, 0, th, in, wb));
+  ADD("packbf_8   8-B NT stores     ", 10.0 * n, hipLaunchKernelGGL(packbf_8<true>, g, b, 0, 0, th, in, wb));
+  ADD("packbf_lds 16-B stores       ", 10.0 * n, hipLaunchKernelGGL(packbf_lds<false>, g, b, 0, 0, th, in, wb));
+  ADD("packbf_lds 16-B NT stores    ", 10.0 * n, hipLaunchKernelGGL(packbf_lds<true>, g, b, 0, 0, th, in, wb));
   for (int r = 0; r < rounds; ++r) {
     for (auto& v : vs) {
       hipLaunchKernelGGL(flush_k, dim3(8192), dim3(T), 0, 0, flush, nf / 4);
