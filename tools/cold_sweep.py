@@ -73,10 +73,17 @@ def main():
         kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True, wire_dtype=wd)
         for e in (two, one, kept):
             e.step()  # steady-state SGD mode from here on
+        scratch = torch.empty_like(two.theta)
         kern = {"delta_pack": (two, two.pseudo_gradient, 8 + wb),
                 "unpack_sgd": (two, two.apply, 20 + wb),
                 "delta_sgd": (one, lambda: one._step(None), 24),
-                "delta_pack_sgd": (kept, lambda: kept._step(None), 24 + wb)}
+                "delta_pack_sgd": (kept, lambda: kept._step(None), 24 + wb),
+                # the sharded step's write-back of θ into the inner params, and the per-step DP
+                # grad sync's pack / average-back (GradSync) on the same tree
+                # (timing only: scratch holds the gathered copy, the average is by 1)
+                "scatter": (two, lambda: two.k.scatter(two.tree, -1, two.theta, 0), 8),
+                "gather": (two, lambda: two.k.gather(two.tree, -1, 0, scratch), 8),
+                "unpack_avg": (two, lambda: two.k.unpack_avg(two.tree, -1, scratch, 1, 0), 8)}
         half = (two.tree.n_chunks + 1) // 2
         # (flags, grid): grid half = two chunks per workgroup (grid-stride walk)
         flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (0, 0): "plain",
