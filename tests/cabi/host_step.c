@@ -4,6 +4,10 @@
  * restatement of src/utils.py:221, src/train.py:267 and src/utils.py:226):
  *   step 1: dl_delta_pack_sgd (one pass, first step, wire kept)
  *   step 2: dl_delta_pack -> dl_unpack_sgd (divisor 1: one peer, src/comm.py:118-119)
+ *   step 3: per bucket dl_delta_pack -> dl_allreduce -> dl_unpack_sgd over a one-rank RCCL
+ *           communicator the library creates (dl_rccl_load, dl_comm_unique_id, dl_comm_init)
+ *   step 4: the sharded step per bucket: dl_delta_pack -> dl_reduce_scatter -> dl_shard_sgd
+ *           -> dl_all_gather -> dl_scatter on the same communicator
  * plus an argument error (unbound slot) reported through the return code and dl_last_error.
  * Built by __graft_entry__.build() (gcc, no GPU needed); run by tests/test_cabi_host_gpu.py.
  * Exit status 0 = every byte equal. */
@@ -95,8 +99,18 @@ int main(void) {
   float* got = malloc(total * 4);
   float* gotm = malloc(total * 4);
   float* gotw = malloc(total * 4);
+  /* steps 3-4: RCCL through the library, one rank (src/comm.py:122 with one peer) */
+  DL(dl_rccl_load(NULL));
+  char id[128];
+  dl_comm_t comm = NULL;
+  DL(dl_comm_unique_id(id));
+  DL(dl_comm_init(&comm, 1, id, 0));
+  float *d_gshard, *d_thshard, *d_momshard; /* this rank's shards: the whole bucket at n = 1 */
+  HIP(hipMalloc((void**)&d_gshard, total * 4));
+  HIP(hipMalloc((void**)&d_thshard, total * 4));
+  HIP(hipMalloc((void**)&d_momshard, total * 4));
   int ok = 1;
-  for (int step = 1; step <= 2; ++step) {
+  for (int step = 1; step <= 4; ++step) {
     /* inner = θ + noise (the synthetic stand-in for H inner steps) */
     for (int t = 0; t < NT; ++t) {
       or_fill_synth(h_in[t], NUMEL[t], (uint64_t)(1000 * step), (uint64_t)t, 0.0f, 1e-3f,
@@ -106,11 +120,33 @@ int main(void) {
     if (step == 1) {
       DL(dl_delta_pack_sgd(tree, DL_ALL_BUCKETS, 0, d_theta, d_wire, DL_F32, d_mom, lr, mom, 1, 1,
                            NULL));
-    } else {
+    } else if (step == 2) {
       for (int32_t b = 0; b < nbkt; ++b) {
         DL(dl_delta_pack(tree, b, 0, d_theta, d_wire, DL_F32, NULL));
         DL(dl_unpack_sgd(tree, b, d_wire, DL_F32, 1, d_theta, d_mom, lr, mom, 1, 0, 0, NULL));
       }
+    } else if (step == 3) {
+      for (int32_t b = 0; b < nbkt; ++b) {
+        int64_t lo = 0, hi = 0;
+        DL(dl_tree_bucket_range(tree, b, &lo, &hi));
+        DL(dl_delta_pack(tree, b, 0, d_theta, d_wire, DL_F32, NULL));
+        DL(dl_allreduce(d_wire + lo, hi - lo, DL_F32, comm, NULL));
+        DL(dl_unpack_sgd(tree, b, d_wire, DL_F32, 1, d_theta, d_mom, lr, mom, 1, 0, 0, NULL));
+      }
+    } else {
+      HIP(hipMemcpy(d_thshard, d_theta, total * 4, hipMemcpyDeviceToDevice));
+      HIP(hipMemcpy(d_momshard, d_mom, total * 4, hipMemcpyDeviceToDevice));
+      for (int32_t b = 0; b < nbkt; ++b) {
+        int64_t lo = 0, hi = 0;
+        DL(dl_tree_bucket_range(tree, b, &lo, &hi));
+        DL(dl_delta_pack(tree, b, 0, d_theta, d_wire, DL_F32, NULL));
+        DL(dl_reduce_scatter(d_wire + lo, d_gshard + lo, hi - lo, DL_F32, comm, NULL));
+        DL(dl_shard_sgd(d_gshard + lo, DL_F32, 1, d_thshard + lo, d_momshard + lo, hi - lo, lr,
+                        mom, 1, 0, NULL));
+        DL(dl_all_gather(d_thshard + lo, d_theta + lo, hi - lo, DL_F32, comm, NULL));
+        DL(dl_scatter(tree, b, d_theta, 0, NULL));
+      }
+      HIP(hipMemcpy(d_mom, d_momshard, total * 4, hipMemcpyDeviceToDevice));
     }
     HIP(hipDeviceSynchronize());
     for (int t = 0; t < NT; ++t) { /* the oracle's step */
@@ -128,6 +164,7 @@ int main(void) {
       ok &= same("inner (sync_inner_model)", t, h_in[t], h_theta[t], NUMEL[t]);
     }
   }
+  DL(dl_comm_destroy(comm));
   DL(dl_tree_destroy(tree));
   printf("cabi host: %d tensors, %lld packed elements, %d buckets, %d chunks: %s\n", NT,
          (long long)total, nbkt, nch, ok ? "bit-exact vs oracle" : "MISMATCH");

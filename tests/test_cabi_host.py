@@ -1,6 +1,8 @@
 """The C-ABI from a non-Python host: tests/cabi/host_step.c (plain C + the HIP runtime +
-libdiloco_hip.so, no Python, no torch) runs two outer steps on a ragged tree and compares
-them bit for bit with the C oracle. On the GPU it must pass; without a GPU it must fail
+libdiloco_hip.so, no Python, no torch) runs four outer steps on a ragged tree -- the one-pass
+kernel, the two-kernel pair, the bucketed all-reduce and the sharded reduce-scatter / shard SGD
+/ all-gather / scatter step over a one-rank RCCL communicator the library creates -- and
+compares them bit for bit with the C oracle. On the GPU it must pass; without a GPU it must fail
 loudly (the library reports hipErrorNoDevice), never succeed silently."""
 import os
 import subprocess
