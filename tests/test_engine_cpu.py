@@ -130,3 +130,82 @@ def test_direct_exchange_arguments():
         ei.pseudo_gradient()
     with pytest.raises(RuntimeError, match="exchange='xgmi'"):
         e.apply()
+
+
+class _CountingKernels(OracleKernels):
+    """The oracle backend, counting pointer-table binds per slot."""
+
+    def __init__(self):
+        super().__init__()
+        self.binds = 0
+
+    def bind(self, tree, slot, tensors, device):
+        self.binds += 1
+        return super().bind(tree, slot, tensors, device)
+
+
+@pytest.mark.parametrize("kind", ["sharded", "tiled", "two_kernel", "int8", "fused"])
+def test_one_bind_per_outer_step(kind):
+    """step() binds the inner slot once, however many buckets the step walks (the per-bucket
+    building blocks only bind when called on their own)."""
+    _, params = _micro_params()
+    k = _CountingKernels()
+    kw = {"sharded": dict(shard=True, fuse_single=False),
+          "tiled": dict(fuse_single=False, tile_chunks=1),
+          "two_kernel": dict(fuse_single=False, tile_chunks=0),
+          "int8": dict(wire_dtype=torch.int8),
+          "fused": dict(fuse_single=True, keep_wire=True)}[kind]
+    e = OuterSync(params, world_size=1, bucket_cap_elems=4096, kernels=k, **kw)
+    assert e.tree.n_buckets > 2
+    for _ in range(3):
+        before = k.binds
+        e.step()
+        assert k.binds - before == 1, kind
+    before = k.binds
+    e.pseudo_gradient(0)  # on its own: binds
+    assert k.binds - before == 1
+
+
+def test_int8_single_replica_whole_tree_equals_per_bucket():
+    """The one-replica int8 step in three whole-tree launches equals the per-bucket sequence
+    (dl_delta_q8 -> dl_q8_reduce -> dl_unpack_sgd_q8 per bucket): at n = 1 no bucket is padded,
+    so the slots of consecutive buckets are the tree's chunks in order."""
+    spec, params_a = _micro_params()
+    _, params_b = _micro_params()
+    a = OuterSync(params_a, world_size=1, bucket_cap_elems=4096, wire_dtype=torch.int8)
+    b = OuterSync(params_b, world_size=1, bucket_cap_elems=4096, wire_dtype=torch.int8)
+    assert a.tree.n_buckets > 2
+    for s in (1, 2):
+        vals = synth.inner_tree([t.numpy().reshape(-1) for t in a.unpacked(a.theta)], s, 0)
+        for pa, pb, v in zip(params_a, params_b, vals):
+            pa.copy_(torch.from_numpy(v).view(pa.shape))
+            pb.copy_(torch.from_numpy(v).view(pb.shape))
+        a.step()
+        for k in range(b.tree.n_buckets):  # the pre-round-2 per-bucket sequence
+            b.pseudo_gradient(k)
+            _nch, m, _ = b.q8_plan[k]
+            region = b.q8_region(k)
+            b.k.q8_reduce(region, 1, m, 1, region)
+            b.apply(k)
+        b.steps_done += 1
+        assert a.theta.numpy().tobytes() == b.theta.numpy().tobytes()
+        assert a.mom.numpy().tobytes() == b.mom.numpy().tobytes()
+        assert a.q_slots.numpy().tobytes() == b.q_slots.numpy().tobytes()
+        assert _flat(params_a).tobytes() == _flat(params_b).tobytes()
+
+
+def test_gradsync_single_replica_without_group_is_identity():
+    """GradSync at one replica with no process group: gather -> identity -> /1 back, every
+    gradient unchanged (the path runs; nothing is exchanged)."""
+    from diloco_amd.gradsync import GradSync
+
+    params = [torch.nn.Parameter(torch.zeros(n)) for n in (1, 3, 5000, 64, 4097)]
+    for i, p in enumerate(params):
+        p.grad = torch.full_like(p, float(i) + 0.25)
+    gs = GradSync(params, None, 1, bucket_cap_elems=4096)
+    assert gs.tree.n_buckets > 1
+    gs.sync()
+    for i, p in enumerate(params):
+        assert torch.equal(p.grad, torch.full_like(p, float(i) + 0.25))
+        o = int(gs.tree.seg_off[i])
+        assert torch.equal(gs.wire[o:o + p.numel()], p.grad)

@@ -184,3 +184,26 @@ def test_copy_kernel_copies_exactly(flags):
         assert bool((dst[4 * n16:] == -1.0).all()), (flags, n16)
     with pytest.raises(_lib.DilocoHipError, match="multiple of 16"):
         _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 20, flags, None)
+
+
+def test_outer_step_called_on_the_engines_own_stream():
+    """A caller already running on the engine's stream (e.g. a loop that does all its outer
+    work under `torch.cuda.stream(engine.stream)`) skips the stream joins; results stay
+    bit-exact against the reference (micro_n1.npz)."""
+    from diloco_amd.outer import OuterSync
+
+    spec = get_tree("micro")
+    g = load_npz("micro_n1.npz")
+    shapes = [s for _, s in spec.params()]
+    params = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
+    e = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True, side_stream=True)
+    assert e.stream is not None
+    with torch.cuda.stream(e.stream):
+        for s in (1, 2):
+            th = [t.reshape(-1) for t in e.unpacked(e.theta)]
+            synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in params])
+            e.step()
+    torch.cuda.synchronize()
+    got = np.concatenate([p.reshape(-1).cpu().numpy() for p in params])
+    assert got.tobytes() == g["theta_s2"].tobytes()
+    e.close()
