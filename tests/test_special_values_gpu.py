@@ -14,6 +14,9 @@ import numpy as np
 import pytest
 import torch
 
+# inf - inf, NaN arithmetic in the host-side inputs is intended
+pytestmark_np = np.seterr(invalid="ignore", over="ignore")
+
 from diloco_amd.outer import OuterSync
 
 pytestmark = pytest.mark.gpu
@@ -153,3 +156,38 @@ def test_special_values_match_torch(variant):
                           where + " wire")
     for e in engines:
         e.close()
+
+
+def test_special_values_int8_wire_match_oracle():
+    """The int8 codec has no reference counterpart: its special-value semantics are the
+    oracle's C restatement (oracle/diloco_oracle.c or_delta_q8 / or_q8_reduce / or_q8_deq:
+    amax by fmaxf, so NaN is ignored by the scale and quantises to -127; an Inf amax gives
+    an Inf scale), matched bit for bit (NaN positions) over two steps."""
+    from oracle import oracle
+
+    theta0 = _host_tree(5, SPECIAL_THETA)
+    b, ps = _device(theta0)
+    e = OuterSync(ps, world_size=1, bucket_cap_elems=4096, wire_dtype=torch.int8)
+    st = oracle.OuterState(theta0)
+    for step in (1, 2):
+        pert = _host_tree(100 * step, SPECIAL_INNER)
+        inner = [(t + p * F(1e-3)).astype(F) if step == 2 else p
+                 for t, p in zip(st.theta, pert)]
+        for dst, x in zip(ps, inner):
+            dst.copy_(torch.from_numpy(x))
+        deltas = [oracle.delta(st.theta[t], inner[t]) for t in range(len(NUMELS))]
+        g = oracle.q8_average([deltas], NUMELS, [c1 - c0 for c0, c1 in e.tree.bucket_chunks])
+        for t in range(len(NUMELS)):
+            if st.buf[t] is None:
+                st.buf[t] = np.empty_like(st.theta[t])
+            oracle.sgd(st.theta[t], st.buf[t], g[t], st.lr, st.momentum, st.nesterov, step == 1)
+        st.steps += 1
+        e.step()
+        torch.cuda.synchronize()
+        th, mom = e.unpacked(e.theta), e.unpacked(e.mom)
+        for t in range(len(NUMELS)):
+            where = f"int8 step {step} tensor {t}"
+            _same(th[t].cpu().numpy(), st.theta[t], where + " theta")
+            _same(mom[t].cpu().numpy(), st.buf[t], where + " momentum")
+            _same(ps[t].cpu().numpy(), st.theta[t], where + " inner")
+    e.close()
