@@ -191,3 +191,20 @@ def test_special_values_int8_wire_match_oracle():
             _same(mom[t].cpu().numpy(), st.buf[t], where + " momentum")
             _same(ps[t].cpu().numpy(), st.theta[t], where + " inner")
     e.close()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_serializer_widens_every_16_bit_pattern_like_torch(dtype):
+    """dl_serialize's payload conversion (src/serializer.py:12-13: torch.cat promotes a bf16 /
+    fp16 payload to the fp32 metadata plane's dtype) over ALL 65,536 bit patterns -- NaNs,
+    infinities, signed zeros, subnormals -- against torch's own .to(torch.float32)."""
+    from diloco_amd.serializer import Serializer
+
+    bits = torch.arange(-32768, 32768, dtype=torch.int32).to(torch.int16)
+    x = bits.view(dtype).reshape(256, 256)
+    framed = Serializer((256, 256)).serialize(x.to(DEV), (7, 11))
+    torch.cuda.synchronize()
+    got = framed[1].cpu().numpy()
+    ref = x.to(torch.float32).numpy()
+    _same(got.reshape(-1), ref.reshape(-1), f"{dtype} payload")
+    assert framed[0].reshape(-1)[:2].tolist() == [7.0, 11.0]
