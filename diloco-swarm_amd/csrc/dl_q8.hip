@@ -154,15 +154,24 @@ struct UnpackSgdQ8 {
       const int nv = ck.len >> 2;
       uint32_t w[kUnroll];
       float4 t[kUnroll], m[kUnroll];
+      // the slot's 4 KB payload arrives as one non-temporal 16-B load per lane, staged in LDS
+      // (tools/gpu_ab_q8.sh: -1 % at T1.3B against four 4-B loads per lane)
+      __shared__ u32x4 stage[DL_CHUNK_ELEMS / 16];
+      const u32x4 qv = __builtin_nontemporal_load((const DL_GLOBAL u32x4*)q + tid);
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
         if (v < nv) {
-          w[u] = ((gcu32)q)[v];
           t[u] = ldf4<NTL>(th, v);
           if (MODE == 2) m[u] = ldf4<NTL>(mb, v);
         }
       }
+      stage[tid] = qv;
+      __syncthreads();
+      const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) w[u] = st32[u * kThreads + tid];
+      __syncthreads();  // `stage` is reused by the workgroup's next chunk
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
