@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(kThreads)
 // one workgroup lands on it; with one workgroup per CU every XCD receives its share under
 // any placement that uses every CU. `xcc` (census, tests): each workgroup records the XCD it
 // ran on (s_getreg HW_REG_XCC_ID; a read, the record is a vector store), which
-// tests/test_fence_gpu.py checks covers all XCDs.
+// tests/test_runtime_gpu.py::test_sys_fence_reaches_every_xcd checks covers all XCDs.
 __global__ void __launch_bounds__(64) k_sys_fence(uint32_t* __restrict__ xcc) {
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");

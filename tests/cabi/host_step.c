@@ -9,7 +9,7 @@
  *   step 4: the sharded step per bucket: dl_delta_pack -> dl_reduce_scatter -> dl_shard_sgd
  *           -> dl_all_gather -> dl_scatter on the same communicator
  * plus an argument error (unbound slot) reported through the return code and dl_last_error.
- * Built by __graft_entry__.build() (gcc, no GPU needed); run by tests/test_cabi_host_gpu.py.
+ * Built by __graft_entry__.build() (gcc, no GPU needed); run by tests/test_cabi_host.py.
  * Exit status 0 = every byte equal. */
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
