@@ -121,11 +121,17 @@ def _sync(ws):
     torch.cuda.synchronize()
 
 
-def kernel_entry(bytes_per_launch, ms, traffic=None, bound="hbm", peak=HBM_PEAK_GBS):
+def kernel_entry(bytes_per_launch, ms, traffic=None, bound="hbm", peak=HBM_PEAK_GBS, rw=None):
+    """rw = (read bytes, read streams, write bytes, write streams) per launch: the kernel's
+    byte mix, read against the same-run read and write ceilings by with_copy_ceiling."""
     ach = bytes_per_launch / (ms * 1e-3) / 1e9
-    return {"bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
-            "frac": round(ach / peak, 4), "traffic": round(traffic) if traffic else None,
-            "bytes_per_launch": bytes_per_launch, "avg_ms": round(ms, 5)}
+    e = {"bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
+         "frac": round(ach / peak, 4), "traffic": round(traffic) if traffic else None,
+         "bytes_per_launch": bytes_per_launch, "avg_ms": round(ms, 5)}
+    if rw is not None:  # (read bytes, read streams, write bytes, write streams)
+        e["read_bytes"], e["read_streams"] = int(rw[0]), int(rw[1])
+        e["write_bytes"], e["write_streams"] = int(rw[2]), int(rw[3])
+    return e
 
 
 SCRUB_MIB = 512  # >= 2 x the 256 MiB Infinity Cache moved per scrub (read 512 + write 512)
@@ -151,42 +157,69 @@ class Scrubber:
         del self.a, self.b
 
 
-def copy_ceiling(dev, mib=1024, reps=10):
-    """What a two-stream copy kernel (dl_copy) moves on this box in this run: read + written
-    bytes / time over `reps` back-to-back copies of `mib` MiB (far beyond the Infinity Cache),
-    default and non-temporal policy, 4 (the walker's shape) and 8 float4 loads in flight per
-    lane; the fastest is the ceiling the roofline fractions are read against beside the 8 TB/s
-    spec peak (boxes differ by ~15 %)."""
+def copy_ceiling(dev, mib=1024, reps=15):
+    """What the memory system gives streaming kernels on this box in this run, `reps` launches
+    back to back over `mib` MiB (far beyond the Infinity Cache), each in the walker's access
+    shape (dl_copy): a two-stream copy -- default and non-temporal policy, 4 (the walker's
+    shape) and 8 float4 loads in flight per lane; the fastest is the copy ceiling the roofline
+    fractions are read against beside the 8 TB/s spec peak (boxes differ by ~15 %) -- and the
+    pure read and pure write rates over 1-4 streams (DL_COPY_READ / DL_COPY_WRITE), which
+    bound a kernel of R bytes read from s_r buffers and W written to s_w at
+    t >= R / read_GBs[s_r] + W / write_GBs[s_w]: the mix ceiling (tools/rw_mix.hip, DESIGN.md
+    §3 -- HBM writes are the slower half). Rates use the median launch."""
     n = (mib << 20) // 4
     a = torch.ones(n, device=dev)
     b = torch.empty(n, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     out = {"bytes_per_copy": 2 * 4 * n}
     nt, wide = _lib.TUNE_NT_LOADS, _lib.COPY_WIDE
-    for name, flags in (("plain", 0), ("nt", nt), ("plain_x8", wide), ("nt_x8", nt | wide)):
-        _lib.call("dl_copy", a.data_ptr(), b.data_ptr(), 4 * n, flags, st)  # warm the launch
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
+
+    def rate(flags, moved, nbytes=4 * n):
+        """moved bytes / the median duration of `reps` back-to-back launches (events on the
+        launching stream around each)"""
+        _lib.call("dl_copy", a.data_ptr(), b.data_ptr(), nbytes, flags, st)  # warm the launch
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        ev[0].record()
         for i in range(reps):
             src, dst = (a, b) if i % 2 == 0 else (b, a)
-            _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 4 * n, flags, st)
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        out[f"{name}_GBs"] = round(2 * 4 * n / (ms * 1e-3) / 1e9, 1)
+            _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), nbytes, flags, st)
+            ev[i + 1].record()
+        ev[-1].synchronize()
+        ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(reps))[reps // 2]
+        return round(moved / (ms * 1e-3) / 1e9, 1)
+
+    for name, flags in (("plain", 0), ("nt", nt), ("plain_x8", wide), ("nt_x8", nt | wide)):
+        out[f"{name}_GBs"] = rate(flags, 2 * 4 * n)
     out["GBs"] = max(v for k, v in out.items() if k.endswith("_GBs"))
+    # pure read / pure write over 1-4 streams (the walker kernels read 1-3 and write 1-4
+    # buffers; default and non-temporal policy, the faster of the two)
+    for kind, flag in (("read", _lib.COPY_READ), ("write", _lib.COPY_WRITE)):
+        out[f"{kind}_GBs"] = {}
+        for k in (1, 2, 3, 4):
+            nb = 4 * n // (16 * k) * (16 * k)  # k equal streams of whole float4s
+            out[f"{kind}_GBs"][k] = max(rate(f | flag | _lib.COPY_STREAMS(k), nb, nb)
+                                        for f in (0, nt))
     del a, b
     torch.cuda.empty_cache()
     return out
 
 
-def with_copy_ceiling(entry, ceiling_gbs):
-    """A kernel_entry with its achieved rate also read against the same-run copy ceiling."""
-    if entry is None or not ceiling_gbs:
+def with_copy_ceiling(entry, ceiling):
+    """A kernel_entry with its achieved rate also read against the same-run copy ceiling and,
+    for an entry that carries its byte mix, the same-run mix ceiling
+    (R + W) / (R / read_GBs + W / write_GBs)."""
+    if entry is None or not isinstance(ceiling, dict) or not ceiling.get("GBs"):
         return entry
     e = dict(entry)
-    e["copy_ceiling"] = ceiling_gbs
-    e["frac_vs_copy"] = round(e["achieved"] / ceiling_gbs, 4)
+    e["copy_ceiling"] = ceiling["GBs"]
+    e["frac_vs_copy"] = round(e["achieved"] / ceiling["GBs"], 4)
+    r, w = e.get("read_bytes"), e.get("write_bytes")
+    rg, wg = ceiling.get("read_GBs"), ceiling.get("write_GBs")
+    if r is not None and rg and wg:
+        sr, sw = e["read_streams"], e["write_streams"]
+        t = (r / rg[sr] if r else 0.0) + (w / wg[sw] if w else 0.0)
+        e["mix_ceiling"] = round((r + w) / t, 1)
+        e["frac_vs_mix"] = round(e["achieved"] * t / (r + w), 4)
     return e
 
 
@@ -251,12 +284,16 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
     fused_name = "delta_pack_sgd" if keep_wire else "delta_sgd"
     # read θ, inner, buf; write θ, buf, inner (+ the wire)
     fused_bytes = (24 + (wb if keep_wire else 0)) * P
+    fused_rw = (12 * P, 3, fused_bytes - 12 * P, 4 if keep_wire else 3)
+    pack_rw, unpack_rw = (8 * P, 2, wb * P, 1), ((wb + 8) * P, 3, 12 * P, 3)
     if single and fuse:
-        res["kernels"] = {fused_name: kernel_entry(fused_bytes, first, pmc.get(fused_name))}
+        res["kernels"] = {fused_name: kernel_entry(fused_bytes, first, pmc.get(fused_name),
+                                                   rw=fused_rw)}
     elif single:
         res["kernels"] = {
-            "delta_pack": kernel_entry((8 + wb) * P, first, pmc.get("delta_pack")),
-            "unpack_sgd": kernel_entry((wb + 20) * P, second, pmc.get("unpack_sgd")),
+            "delta_pack": kernel_entry((8 + wb) * P, first, pmc.get("delta_pack"), rw=pack_rw),
+            "unpack_sgd": kernel_entry((wb + 20) * P, second, pmc.get("unpack_sgd"),
+                                       rw=unpack_rw),
         }
     else:
         res["step_ms_instrumented"] = round(first, 4)
@@ -292,13 +329,13 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
                                "outside the events); step = the kernels' event span, no "
                                "inter-step gap (compare warm_step_ms, not the headline)"}
         if fuse:
-            res["cold"]["kernels"] = {fused_name: kernel_entry(fused_bytes, c_first)}
+            res["cold"]["kernels"] = {fused_name: kernel_entry(fused_bytes, c_first, rw=fused_rw)}
         elif tiled:
             res["cold"]["kernels"] = {}  # tile-interleaved launches: the step only
         else:
             res["cold"]["kernels"] = {
-                "delta_pack": kernel_entry((8 + wb) * P, c_first),
-                "unpack_sgd": kernel_entry((wb + 20) * P, c_second)}
+                "delta_pack": kernel_entry((8 + wb) * P, c_first, rw=pack_rw),
+                "unpack_sgd": kernel_entry((wb + 20) * P, c_second, rw=unpack_rw)}
     # the same kernels back to back (cold inputs: no Infinity-Cache reuse across kernels)
     reps = max(steps, 10)
 
@@ -313,10 +350,13 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
 
     if b2b_loops and single and fuse:
         res["kernels_b2b"] = {fused_name: kernel_entry(fused_bytes,
-                                                        b2b(lambda: eng._step(None)))}
+                                                        b2b(lambda: eng._step(None)),
+                                                        rw=fused_rw)}
     elif b2b_loops and not (eng.sharded or eng.xgmi):
-        res["kernels_b2b"] = {"delta_pack": kernel_entry((8 + wb) * P, b2b(eng.pseudo_gradient)),
-                              "unpack_sgd": kernel_entry((wb + 20) * P, b2b(eng.apply))}
+        res["kernels_b2b"] = {"delta_pack": kernel_entry((8 + wb) * P, b2b(eng.pseudo_gradient),
+                                                         rw=pack_rw),
+                              "unpack_sgd": kernel_entry((wb + 20) * P, b2b(eng.apply),
+                                                         rw=unpack_rw)}
     if single:
         ks = res["kernels"]
         dom = max(ks, key=lambda k: ks[k]["avg_ms"])
@@ -630,9 +670,12 @@ def run_q8(spec, dev, ws, rank, steps, warmup, cap):
         ms = [t / steps for t in tot]
         pmc = load_pmc(spec.name)  # the same whole-tree launches (tools/kernel_driver.py)
         res["kernels"] = {
-            "delta_q8": kernel_entry(8 * P + slot_bytes, ms[0], pmc.get("delta_q8")),
-            "q8_reduce": kernel_entry(2 * slot_bytes, ms[1], pmc.get("q8_reduce")),
-            "unpack_sgd_q8": kernel_entry(slot_bytes + 20 * P, ms[2], pmc.get("unpack_sgd_q8")),
+            "delta_q8": kernel_entry(8 * P + slot_bytes, ms[0], pmc.get("delta_q8"),
+                                     rw=(8 * P, 2, slot_bytes, 1)),
+            "q8_reduce": kernel_entry(2 * slot_bytes, ms[1], pmc.get("q8_reduce"),
+                                      rw=(slot_bytes, 1, slot_bytes, 1)),
+            "unpack_sgd_q8": kernel_entry(slot_bytes + 20 * P, ms[2], pmc.get("unpack_sgd_q8"),
+                                          rw=(slot_bytes + 8 * P, 3, 12 * P, 3)),
         }
     eng.close()
     del eng
@@ -1242,18 +1285,17 @@ def main():
     if not a.only_headline:
         ceiling = _guard(copy_ceiling, dev)
         log(f"copy ceiling {ceiling}")
-    cgbs = ceiling.get("GBs") if isinstance(ceiling, dict) else None
     roof = main_res["roofline"]
     if ws == 1:
-        roof = with_copy_ceiling(roof, cgbs)
+        roof = with_copy_ceiling(roof, ceiling)
     cold = main_res.get("cold")
     roof_cold = None
     if cold:
         ks = cold["kernels"]
         dom = max(ks, key=lambda k: ks[k]["avg_ms"])
-        roof_cold = dict(with_copy_ceiling(ks[dom], cgbs), kernel=dom)
+        roof_cold = dict(with_copy_ceiling(ks[dom], ceiling), kernel=dom)
         cold = dict(cold, value=round(cold["value"], 3), warm_value=round(cold["warm_value"], 3),
-                    kernels={k: with_copy_ceiling(v, cgbs) for k, v in ks.items()})
+                    kernels={k: with_copy_ceiling(v, ceiling) for k, v in ks.items()})
     em.line = {
         "metric": METRIC,
         "value": round(main_res["value"], 3),
@@ -1433,6 +1475,15 @@ def main():
                                                           "rccl_env", env)
                 log(f"rccl_env_{name} done at {em.elapsed():.1f} s")
     em.running = "teardown"
+    # every side leg's kernels read against the same-run copy and mix ceilings too
+    for v in extra.values():
+        if isinstance(v, dict):
+            for key in ("kernels", "kernels_b2b"):
+                if isinstance(v.get(key), dict):
+                    v[key] = {k: with_copy_ceiling(e, ceiling) for k, e in v[key].items()}
+            if isinstance(v.get("cold"), dict) and isinstance(v["cold"].get("kernels"), dict):
+                v["cold"]["kernels"] = {k: with_copy_ceiling(e, ceiling)
+                                        for k, e in v["cold"]["kernels"].items()}
     em.line["wall_s"] = round(em.elapsed(), 1)
     em.emit()
     if dist.is_initialized():

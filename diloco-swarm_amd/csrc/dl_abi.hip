@@ -581,13 +581,30 @@ DL_API int dl_sys_fence_census(uint32_t* xcc, int32_t cap, int32_t* grid, dl_str
 DL_API int dl_copy(const void* src, void* dst, int64_t bytes, int32_t flags, dl_stream_t s) {
   if (bytes < 0 || bytes % 16) return fail(DL_E_ARG, "dl_copy: bytes %lld (multiple of 16)",
                                            (long long)bytes);
+  if (flags & ~(DL_TUNE_NT_LOADS | DL_COPY_WIDE | DL_COPY_READ | DL_COPY_WRITE | (3 << 8)))
+    return fail(DL_E_ARG, "dl_copy: flags 0x%x", flags);
+  const bool rd = (flags & DL_COPY_READ) != 0, wr = (flags & DL_COPY_WRITE) != 0;
+  const bool nt = (flags & DL_TUNE_NT_LOADS) != 0;
+  if (rd && wr) return fail(DL_E_ARG, "dl_copy: DL_COPY_READ and DL_COPY_WRITE together");
+  if (rd || wr) {
+    if (flags & DL_COPY_WIDE) return fail(DL_E_ARG, "dl_copy: DL_COPY_WIDE with a probe");
+    const int streams = ((flags >> 8) & 3) + 1;
+    if (bytes % (16 * streams))
+      return fail(DL_E_ARG, "dl_copy: bytes %lld not a multiple of 16 x %d streams",
+                  (long long)bytes, streams);
+    if (bytes == 0) return DL_OK;
+    if (rd) DL_TRY(check_packed(src, "dl_copy", "src"));
+    else DL_TRY(check_packed(dst, "dl_copy", "dst"));
+    hipError_t e = dl::launch_probe(wr, streams, src, dst, bytes / 16 / streams, nt,
+                                    static_cast<hipStream_t>(s));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "dl_copy");
+  }
+  if (flags & (3 << 8)) return fail(DL_E_ARG, "dl_copy: DL_COPY_STREAMS needs a probe");
   if (bytes == 0) return DL_OK;
   DL_TRY(check_packed(src, "dl_copy", "src"));
   DL_TRY(check_packed(dst, "dl_copy", "dst"));
-  if (flags & ~(DL_TUNE_NT_LOADS | DL_COPY_WIDE))
-    return fail(DL_E_ARG, "dl_copy: flags 0x%x", flags);
-  hipError_t e = dl::launch_copy(src, dst, bytes / 16, (flags & DL_TUNE_NT_LOADS) != 0,
-                                 (flags & DL_COPY_WIDE) != 0, static_cast<hipStream_t>(s));
+  hipError_t e = dl::launch_copy(src, dst, bytes / 16, nt, (flags & DL_COPY_WIDE) != 0,
+                                 static_cast<hipStream_t>(s));
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_copy");
 }
 

@@ -88,5 +88,7 @@ hipError_t launch_resolve_chunks(const Chunk* chunks, const int64_t* loff, const
 // policy, wide = 8 instead of 4 float4 loads in flight per lane
 hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, bool wide,
                        hipStream_t s);
+hipError_t launch_probe(bool write, int streams, const void* src, void* dst, int64_t per16,
+                        bool nt, hipStream_t s);
 
 }  // namespace dl

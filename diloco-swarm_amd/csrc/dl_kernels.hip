@@ -450,6 +450,53 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+// Read and write probes (bench.py's mix ceiling, tools/rw_mix.hip): the buffer is S equal
+// streams and workgroup t touches tile t (4 float4 per lane) of every stream, as a walker
+// kernel with S input (or output) buffers does. The read probe's store is guarded by `sink`,
+// which the host passes as 0: the loads stay live and nothing is written. The write probe sets
+// every 32-bit word to its index.
+template <bool NT, int S>
+__global__ void __launch_bounds__(kThreads)
+    k_probe_read(const float* __restrict__ src, int64_t per16, int32_t sink, float* __restrict__ out) {
+  const int64_t base = int64_t(blockIdx.x) * (kThreads * kUnroll);
+  const int64_t rem = per16 - base;
+  float4 x[S][kUnroll];
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + int(threadIdx.x);
+      if (v < rem) x[k][u] = ldf4<NT>(src + (k * per16 + base) * 4, v);
+    }
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + int(threadIdx.x);
+      if (v < rem) acc += x[k][u].x + x[k][u].y + x[k][u].z + x[k][u].w;
+    }
+  if (sink) out[threadIdx.x] = acc;
+}
+
+template <bool NT, int S>
+__global__ void __launch_bounds__(kThreads)
+    k_probe_write(float* __restrict__ dst, int64_t per16) {
+  const int64_t base = int64_t(blockIdx.x) * (kThreads * kUnroll);
+  const int64_t rem = per16 - base;
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + int(threadIdx.x);
+      const uint32_t w = uint32_t(k * per16 + base + v) * 4u;
+      if (v < rem)
+        stf4<NT>(dst + (k * per16 + base) * 4, v,
+                 make_float4(__uint_as_float(w), __uint_as_float(w + 1), __uint_as_float(w + 2),
+                             __uint_as_float(w + 3)));
+    }
+}
+
 }  // namespace
 
 // ---- launchers -------------------------------------------------------------------------------
@@ -478,6 +525,38 @@ hipError_t launch_copy(const void* src, void* dst, int64_t n16, bool nt, bool wi
   if (n16 <= 0) return hipSuccess;
   if (wide) return nt ? copy_u<true, 8>(src, dst, n16, s) : copy_u<false, 8>(src, dst, n16, s);
   return nt ? copy_u<true, 4>(src, dst, n16, s) : copy_u<false, 4>(src, dst, n16, s);
+}
+
+template <bool NT, int S>
+static hipError_t probe_s(bool write, const void* src, void* dst, int64_t per16, hipStream_t s) {
+  const int64_t per = kThreads * kUnroll;
+  const int64_t grid = (per16 + per - 1) / per;
+  if (grid > INT32_MAX) return hipErrorInvalidValue;
+  if (write)
+    hipLaunchKernelGGL((k_probe_write<NT, S>), dim3(uint32_t(grid)), dim3(kThreads), 0, s,
+                       static_cast<float*>(dst), per16);
+  else
+    hipLaunchKernelGGL((k_probe_read<NT, S>), dim3(uint32_t(grid)), dim3(kThreads), 0, s,
+                       static_cast<const float*>(src), per16, 0, static_cast<float*>(dst));
+  return hipGetLastError();
+}
+
+template <bool NT>
+static hipError_t probe_nt(bool write, int streams, const void* src, void* dst, int64_t per16,
+                           hipStream_t s) {
+  switch (streams) {
+    case 1: return probe_s<NT, 1>(write, src, dst, per16, s);
+    case 2: return probe_s<NT, 2>(write, src, dst, per16, s);
+    case 3: return probe_s<NT, 3>(write, src, dst, per16, s);
+    default: return probe_s<NT, 4>(write, src, dst, per16, s);
+  }
+}
+
+hipError_t launch_probe(bool write, int streams, const void* src, void* dst, int64_t per16,
+                        bool nt, hipStream_t s) {
+  if (per16 <= 0) return hipSuccess;
+  return nt ? probe_nt<true>(write, streams, src, dst, per16, s)
+            : probe_nt<false>(write, streams, src, dst, per16, s);
 }
 
 hipError_t launch_delta_pack(const Launch& L, int inner_slot, const float* outer, void* wire,

@@ -25,7 +25,13 @@ IPC_HANDLE_BYTES = 64
 DL_F32, DL_BF16, DL_F16, DL_U8 = 0, 1, 2, 3
 TUNE_NT_LOADS, TUNE_NT_STORES, TUNE_REVERSE = 1, 2, 4
 TUNE_AUTO = -1
-COPY_WIDE = 8
+COPY_WIDE, COPY_READ, COPY_WRITE = 8, 16, 32
+
+
+def COPY_STREAMS(s: int) -> int:
+    """DL_COPY_STREAMS(s): the read / write probe over s equal streams (1..4)."""
+    return ((s - 1) & 3) << 8
+
 
 _i32, _i64, _u64, _f32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
 _vp = ctypes.c_void_p

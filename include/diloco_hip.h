@@ -305,8 +305,17 @@ DL_API int dl_xgmi_delta_sgd(const uint64_t* inners, const uint64_t* thetas, int
  * workgroup per 16 KiB, 4 float4 loads per lane before the stores); flags: DL_TUNE_NT_LOADS =
  * non-temporal loads and stores, DL_COPY_WIDE = 8 float4 loads per lane (32 KiB per
  * workgroup). bench.py times every variant in the same run as the outer step and reads its
- * roofline fractions against the fastest: the copy ceiling (not on the reference's path). */
+ * roofline fractions against the fastest: the copy ceiling (not on the reference's path).
+ * Probes: DL_COPY_READ only reads src[0:bytes) (dst is not written, may be NULL);
+ * DL_COPY_WRITE only writes dst[0:bytes), each 32-bit word its own index (src unused, may be
+ * NULL). DL_COPY_STREAMS(s), s = 1..4, splits the buffer into s equal streams (bytes a
+ * multiple of 16 s) and has each workgroup touch one 16 KiB tile of every stream, as a walker
+ * kernel with s input (output) buffers does. bench.py combines the rates into the same-run
+ * ceiling of a kernel's byte mix: t >= R / BW_read(s_r) + W / BW_write(s_w) (tools/rw_mix.hip). */
 #define DL_COPY_WIDE 8
+#define DL_COPY_READ 16
+#define DL_COPY_WRITE 32
+#define DL_COPY_STREAMS(s) ((((s) - 1) & 3) << 8)
 DL_API int dl_copy(const void* src, void* dst, int64_t bytes, int32_t flags, dl_stream_t stream);
 
 DL_API const char* dl_last_error(void);

@@ -37,6 +37,8 @@ def test_header_constants_match_python_mirror():
     src = open(HEADER).read()
     consts = dict(re.findall(r"#define (DL_\w+) \(?(-?\d+)\)?", src))
     assert int(consts["DL_TUNE_AUTO"]) == _lib.TUNE_AUTO
+    assert (int(consts["DL_COPY_WIDE"]), int(consts["DL_COPY_READ"]),
+            int(consts["DL_COPY_WRITE"])) == (_lib.COPY_WIDE, _lib.COPY_READ, _lib.COPY_WRITE)
     assert int(consts["DL_ALIGN_ELEMS"]) == _lib.ALIGN_ELEMS
     assert int(consts["DL_CHUNK_ELEMS"]) == _lib.CHUNK_ELEMS
     assert int(consts["DL_MAX_SLOTS"]) == _lib.MAX_SLOTS

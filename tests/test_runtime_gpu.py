@@ -186,6 +186,38 @@ def test_copy_kernel_copies_exactly(flags):
         _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 20, flags, None)
 
 
+@pytest.mark.parametrize("nt", [0, 1])
+@pytest.mark.parametrize("streams", [1, 2, 3, 4])
+def test_copy_kernel_read_and_write_probes(nt, streams):
+    """The read-only and write-only probes of dl_copy over 1-4 streams (bench.py's mix
+    ceiling): DL_COPY_READ writes nothing (dst may be NULL); DL_COPY_WRITE sets each 32-bit
+    word of dst[0:bytes) to its index and nothing past the end (src may be NULL)."""
+    st = torch.cuda.current_stream().cuda_stream
+    f = nt | _lib.COPY_STREAMS(streams)
+    for per16 in (1, 1023, 1024, 2049, 1 << 16):
+        n16 = per16 * streams
+        src = torch.arange(4 * n16, dtype=torch.float32, device=DEV)
+        dst = torch.full((4 * n16 + 64,), -1.0, device=DEV)
+        _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 16 * n16, f | _lib.COPY_READ, st)
+        _lib.call("dl_copy", src.data_ptr(), None, 16 * n16, f | _lib.COPY_READ, st)
+        torch.cuda.synchronize()
+        assert bool((dst == -1.0).all()), (nt, streams, per16)
+        _lib.call("dl_copy", None, dst.data_ptr(), 16 * n16, f | _lib.COPY_WRITE, st)
+        torch.cuda.synchronize()
+        idx = torch.arange(4 * n16, dtype=torch.int32, device=DEV)
+        assert torch.equal(dst[:4 * n16].view(torch.int32), idx), (nt, streams, per16)
+        assert bool((dst[4 * n16:] == -1.0).all()), (nt, streams, per16)
+    with pytest.raises(_lib.DilocoHipError, match="together"):
+        _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 16 * streams,
+                  f | _lib.COPY_READ | _lib.COPY_WRITE, None)
+    if streams > 1:
+        with pytest.raises(_lib.DilocoHipError, match="streams"):
+            _lib.call("dl_copy", src.data_ptr(), None, 16 * streams + 16, f | _lib.COPY_READ,
+                      None)
+        with pytest.raises(_lib.DilocoHipError, match="needs a probe"):
+            _lib.call("dl_copy", src.data_ptr(), dst.data_ptr(), 16 * streams, f, None)
+
+
 def test_outer_step_called_on_the_engines_own_stream():
     """A caller already running on the engine's stream (e.g. a loop that does all its outer
     work under `torch.cuda.stream(engine.stream)`) skips the stream joins; results stay
