@@ -96,6 +96,7 @@ struct dl_tree_s {
   std::vector<uint8_t> slot_aligned;
   int32_t grid = 0;                 // 0 = one workgroup per chunk
   int32_t flags = DL_TUNE_AUTO;
+  int32_t slot_period = 0, slot_read = 0;  // dl_tree_slot (0 = off)
 };
 
 extern "C" {
@@ -273,6 +274,17 @@ DL_API int dl_tree_tune(dl_tree_t t, int32_t max_blocks, int32_t flags) {
   return DL_OK;
 }
 
+DL_API int dl_tree_slot(dl_tree_t t, int32_t period_ticks, int32_t read_ticks) {
+  if (!t) return fail(DL_E_ARG, "dl_tree_slot: null tree");
+  if (period_ticks < 0 || read_ticks < 0 || (period_ticks > 0 && read_ticks >= period_ticks) ||
+      period_ticks > 1000000)
+    return fail(DL_E_ARG, "dl_tree_slot: period %d, read %d ticks (0 <= read < period <= 10^6)",
+                period_ticks, read_ticks);
+  t->slot_period = period_ticks;
+  t->slot_read = period_ticks > 0 ? read_ticks : 0;
+  return DL_OK;
+}
+
 DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t n,
                         dl_stream_t stream) {
   if (!t) return fail(DL_E_ARG, "dl_tree_bind: null tree");
@@ -348,6 +360,8 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
   L->grid = t->grid;
   L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
   L->stream = static_cast<hipStream_t>(s);
+  L->slot_period = t->slot_period;
+  L->slot_read = t->slot_read;
   return DL_OK;
 }
 

@@ -1,6 +1,8 @@
 // Device-side building blocks shared by the kernel translation units (dl_kernels.hip,
 // dl_q8.hip): streaming memory ops, element conversions, the segment walker and its launcher.
 #pragma once
+#include <type_traits>
+
 #include "dl_internal.h"
 
 namespace dl {
@@ -152,8 +154,79 @@ __device__ __forceinline__ void sgd1(float g, float& buf, float& th, const SgdAr
   }
 }
 
+// ---- clock-slotted walker (dl_tree_slot) ----------------------------------------------------
+// HBM serves a streaming kernel's reads at ~7 TB/s and its writes at 5.5-6.9, but the steady
+// mix of both that a one-workgroup-per-chunk walker produces runs ~10 % below the time the
+// reads and the writes take separately (tools/rw_mix.hip). The slotted walker
+// separates them in time without any communication between workgroups: a resident grid, each
+// workgroup aligning its rounds to absolute slots of the chip's 100 MHz real-time counter
+// (s_memrealtime) -- all loads of a round issued at the slot's start, all stores `read` ticks
+// later -- so the whole chip reads, then writes. A workgroup behind schedule goes at once
+// instead of skipping a slot; every wait ends when the counter passes a target at most one
+// period ahead. Results do not depend on the timing (same arithmetic, same stores).
+__device__ __forceinline__ uint64_t rtc() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void wait_until(uint64_t t) {
+  while (rtc() < t) __builtin_amdgcn_s_sleep(2);
+  __asm__ volatile("" ::: "memory");
+}
+
+// called by a body between its loads (and arithmetic) and its stores
+struct NoGate {
+  __device__ __forceinline__ void operator()() const {}
+};
+struct SlotGate {
+  uint64_t t;
+  __device__ __forceinline__ void operator()() const {
+    __asm__ volatile("" ::: "memory");
+    wait_until(t);
+  }
+};
+
+template <class Body, bool NTL, bool NTS>
+__global__ void __launch_bounds__(kThreads)
+    k_walk_slotted(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1,
+                   void* const* __restrict__ caddr, int32_t nchunk, uint32_t period,
+                   uint32_t read, Body body) {
+  uint64_t slot = (rtc() / period + 1) * period;
+  for (int32_t i = int32_t(blockIdx.x); i < c1 - c0; i += int32_t(gridDim.x), slot += period) {
+    const int32_t c = c0 + i;
+    const Chunk ck = chunks[c];
+    wait_until(slot);
+    body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x), SlotGate{slot + read});
+  }
+}
+
+// workgroups of k that fit on the device at once (the slotted walker's grid)
+template <class K>
+int32_t resident_grid(K kernel) {
+  int per_cu = 0, cus = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess)
+    return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return per_cu * cus;
+}
+
+// bodies that take a gate between their loads and their stores declare kSlotted = true
+template <class B, class = void>
+struct slotted : std::false_type {};
+template <class B>
+struct slotted<B, std::void_t<decltype(B::kSlotted)>> : std::bool_constant<B::kSlotted> {};
+
 template <class Body, bool NTL, bool NTS>
 hipError_t run_policy(const Launch& L, const Body& body, int32_t grid) {
+  if constexpr (slotted<Body>::value) {
+    if (L.slot_period > 0) {
+      static const int32_t resident = resident_grid(k_walk_slotted<Body, NTL, NTS>);
+      const int32_t n = L.c1 - L.c0;
+      const int32_t g = resident > 0 && resident < n ? resident : n;
+      hipLaunchKernelGGL((k_walk_slotted<Body, NTL, NTS>), dim3(g), dim3(kThreads), 0, L.stream,
+                         L.chunks, L.c0, L.c1, L.caddr, L.nchunk, uint32_t(L.slot_period),
+                         uint32_t(L.slot_read), body);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((k_walk<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream, L.chunks,
                      L.c0, L.c1, L.caddr, L.nchunk, (L.flags & DL_TUNE_REVERSE) ? 1 : 0, body);
   return hipGetLastError();

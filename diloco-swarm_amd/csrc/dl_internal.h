@@ -39,6 +39,10 @@ struct Launch {
   int32_t grid;   // 0 = one workgroup per chunk
   int32_t flags;  // DL_TUNE_*
   hipStream_t stream;
+  // clock-slotted launch (dl_tree_slot; 0 = off): a resident grid whose rounds start every
+  // slot_period ticks of the 100 MHz real-time counter, stores slot_read ticks after the loads
+  int32_t slot_period;
+  int32_t slot_read;
 };
 
 // peers of the direct exchange (dl_xgmi.hip): each rank's packed wire and θ, IPC-mapped

@@ -28,8 +28,10 @@ struct DeltaPack {
   int inner_slot;
   const float* outer;
   W* wire;
-  template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+  static constexpr bool kSlotted = true;
+  template <bool NTL, bool NTS, class G = NoGate>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
+                                      const G& gate = G()) const {
     const float* in = slot_ptr<const float>(caddr, nchunk, inner_slot, c);
     const float* th = outer + ck.poff;
     W* w = wire + ck.poff;
@@ -44,6 +46,7 @@ struct DeltaPack {
           b[u] = ldf4<NTL>(in, v);
         }
       }
+      gate();
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
@@ -52,6 +55,7 @@ struct DeltaPack {
       const int i = (nv << 2) + tid;
       if (i < ck.len) WireIO<W>::st1(w, i, th[i] - in[i]);
     } else {
+      gate();
       for (int i = tid; i < ck.len; i += kThreads) WireIO<W>::st1(w, i, th[i] - in[i]);
     }
   }
@@ -103,8 +107,10 @@ struct UnpackSgd {
   float d;
   SgdArgs a;
   int inner_slot;
-  template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+  static constexpr bool kSlotted = true;
+  template <bool NTL, bool NTS, class G = NoGate>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
+                                      const G& gate = G()) const {
     float* in = inner_slot >= 0 ? slot_ptr<float>(caddr, nchunk, inner_slot, c) : nullptr;
     const W* w = wire + ck.poff;
     float* th = outer + ck.poff;
@@ -129,6 +135,7 @@ struct UnpackSgd {
         sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
         sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
       }
+      gate();
       store_rows<NTS>(th, t, nv, tid);
       if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
       if (in) store_rows<NTS>(in, t, nv, tid);
@@ -143,6 +150,7 @@ struct UnpackSgd {
         if (in) in[i] = t1;
       }
     } else {
+      gate();
       for (int i = tid; i < ck.len; i += kThreads) {
         float gg = WireIO<W>::ld1(w, i);
         if (DIV) gg = gg / d;
@@ -165,8 +173,10 @@ struct DeltaSgd {
   float* mom;
   SgdArgs a;
   int inner_slot;
-  template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+  static constexpr bool kSlotted = true;
+  template <bool NTL, bool NTS, class G = NoGate>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
+                                      const G& gate = G()) const {
     float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
     float* th = outer + ck.poff;
     float* mb = mom + ck.poff;
@@ -190,6 +200,7 @@ struct DeltaSgd {
         sgd1<MODE>(g.z, m[u].z, t[u].z, a);
         sgd1<MODE>(g.w, m[u].w, t[u].w, a);
       }
+      gate();
       store_rows<NTS>(th, t, nv, tid);
       if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
       store_rows<NTS>(in, t, nv, tid);
@@ -203,6 +214,7 @@ struct DeltaSgd {
         in[i] = t1;
       }
     } else {
+      gate();
       for (int i = tid; i < ck.len; i += kThreads) {
         const float g = th[i] - in[i];
         float b = (MODE == 2) ? mb[i] : 0.f, t1 = th[i];
@@ -232,8 +244,10 @@ struct DeltaPackSgd {
     if constexpr (sizeof(W) == 2) return bf2f(f2bf(g));
     else return g;
   }
-  template <bool NTL, bool NTS>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+  static constexpr bool kSlotted = true;
+  template <bool NTL, bool NTS, class G = NoGate>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
+                                      const G& gate = G()) const {
     float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
     float* th = outer + ck.poff;
     float* mb = mom + ck.poff;
@@ -260,6 +274,7 @@ struct DeltaPackSgd {
         sgd1<MODE>(g.z, m[u].z, t[u].z, a);
         sgd1<MODE>(g.w, m[u].w, t[u].w, a);
       }
+      gate();
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
@@ -280,6 +295,7 @@ struct DeltaPackSgd {
         in[i] = t1;
       }
     } else {
+      gate();
       for (int i = tid; i < ck.len; i += kThreads) {
         const float g0 = th[i] - in[i];
         WireIO<W>::st1(w, i, g0);

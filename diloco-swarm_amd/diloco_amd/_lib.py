@@ -52,6 +52,7 @@ SIGNATURES = {
     "dl_tree_bucket_chunks": (ctypes.c_int, [_vp, _i32, _pi32, _pi32]),
     "dl_tree_bind": (ctypes.c_int, [_vp, _i32, _pu64, _i32, _vp]),
     "dl_tree_tune": (ctypes.c_int, [_vp, _i32, _i32]),
+    "dl_tree_slot": (ctypes.c_int, [_vp, _i32, _i32]),
     "dl_delta_pack": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _vp]),
     "dl_unpack_avg": (ctypes.c_int, [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp]),
     "dl_unpack_sgd": (

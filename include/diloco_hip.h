@@ -111,6 +111,14 @@ DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, 
 #define DL_TUNE_AUTO (-1)
 DL_API int dl_tree_tune(dl_tree_t tree, int32_t max_blocks, int32_t flags);
 
+/* Clock-slotted launches of the tree's SGD and delta kernels (dl_delta_pack_sgd,
+ * dl_delta_sgd, dl_unpack_sgd, dl_delta_pack): a grid of as many workgroups as fit on the GPU
+ * at once, whose rounds (one chunk per workgroup) start every period_ticks ticks of the GPU's
+ * 100 MHz real-time counter, the stores of a round read_ticks after its loads -- the chip reads,
+ * then writes, instead of a steady mix. period_ticks = 0 (the default) turns it
+ * off. Results are identical either way; only the timing changes. */
+DL_API int dl_tree_slot(dl_tree_t tree, int32_t period_ticks, int32_t read_ticks);
+
 /* ---- hot-path kernels ----------------------------------------------------------------- */
 
 /* a2: compute_pseudo_gradient, src/utils.py:218-221:

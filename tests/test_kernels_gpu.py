@@ -340,6 +340,57 @@ def test_delta_pack_sgd_equals_two_kernel_pair(wire, momentum, nesterov, misalig
             assert p.cpu().numpy().tobytes() == q.cpu().numpy().tobytes()
 
 
+@pytest.mark.parametrize("kernel", ["delta_pack_sgd", "delta_sgd", "two_kernel"])
+@pytest.mark.parametrize("period,read", [(2, 1), (3000, 1140), (20000, 7600)])
+@pytest.mark.parametrize("misaligned", [False, True])
+def test_slotted_launches_are_bit_identical(kernel, period, read, misaligned):
+    """dl_tree_slot (a resident grid whose rounds follow the GPU's real-time counter) changes
+    only the timing: θ, momentum, the wire and the inner params equal the plain walker's bit
+    for bit -- with more chunks than resident workgroups (several rounds each), ragged tails,
+    the scalar path, a period so short that every round is late and one far longer than a
+    round."""
+    sizes = RAGGED + [2500 * 4096 + 77]
+    g0 = torch.Generator().manual_seed(31)
+    host = [torch.randn(n, generator=g0) for n in sizes]
+
+    def place():
+        if not misaligned:
+            return [h.to(DEV) for h in host]
+        base = torch.empty(sum(sizes) + len(sizes), device=DEV)
+        out, o = [], 1
+        for h in host:
+            out.append(base[o:o + h.numel()])
+            out[-1].copy_(h)
+            o += h.numel() + 1
+        return out
+
+    kw = {"delta_pack_sgd": dict(fuse_single=True, keep_wire=True),
+          "delta_sgd": dict(fuse_single=True),
+          "two_kernel": dict(fuse_single=False, tile_chunks=0)}[kernel]
+    pa, pb = place(), place()
+    ea = OuterSync(pa, world_size=1, **kw)
+    eb = OuterSync(pb, world_size=1, **kw)
+    ea.tree.slot(period, read)
+    for _ in range(2):
+        noise = [torch.randn(n, generator=g0).to(DEV) * 1e-3 for n in sizes]
+        for p, q, z in zip(pa, pb, noise):
+            p.add_(z)
+            q.add_(z)
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(ea.theta.view(torch.int32), eb.theta.view(torch.int32))
+        assert torch.equal(ea.mom.view(torch.int32), eb.mom.view(torch.int32))
+        if ea.wire is not None and kernel != "delta_sgd":
+            assert torch.equal(ea.wire.view(torch.int32), eb.wire.view(torch.int32))
+        for p, q in zip(pa, pb):
+            assert torch.equal(p.view(torch.int32), q.view(torch.int32))
+    with pytest.raises(_lib.DilocoHipError, match="period"):
+        ea.tree.slot(100, 100)
+    ea.close()
+    eb.close()
+
+
 def test_delta_pack_sgd_micro_matches_reference():
     """The one-pass step with the wire kept reproduces the reference's outer steps AND its
     outer.grad (the wire holds delta_s{s}_r0 after step s), micro tree, n = 1."""
