@@ -159,9 +159,9 @@ __device__ __forceinline__ void sgd1(float g, float& buf, float& th, const SgdAr
 // mix of both that a one-workgroup-per-chunk walker produces runs ~10 % below the time the
 // reads and the writes take separately (tools/rw_mix.hip). The slotted walker
 // separates them in time without any communication between workgroups: a resident grid, each
-// workgroup aligning its rounds to absolute slots of the chip's 100 MHz real-time counter
-// (s_memrealtime) -- all loads of a round issued at the slot's start, all stores `read` ticks
-// later -- so the whole chip reads, then writes. A workgroup behind schedule goes at once
+// workgroup pacing its rounds by the chip's 100 MHz real-time counter (s_memrealtime) from its
+// own start -- all loads of a round issued at the round's start, all stores `read` ticks
+// later, the next round `period` ticks after the last -- so the whole chip reads, then writes. A workgroup behind schedule goes at once
 // instead of skipping a slot; every wait ends when the counter passes a target at most one
 // period ahead. Results do not depend on the timing (same arithmetic, same stores).
 __device__ __forceinline__ uint64_t rtc() { return __builtin_amdgcn_s_memrealtime(); }
@@ -187,7 +187,9 @@ __global__ void __launch_bounds__(kThreads)
     k_walk_slotted(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1,
                    void* const* __restrict__ caddr, int32_t nchunk, uint32_t period,
                    uint32_t read, Body body) {
-  uint64_t slot = (rtc() / period + 1) * period;
+  // the first round starts at once: the resident grid is dispatched within a few us, so the
+  // workgroups' own start times already agree to a small fraction of a period
+  uint64_t slot = rtc();
   for (int32_t i = int32_t(blockIdx.x); i < c1 - c0; i += int32_t(gridDim.x), slot += period) {
     const int32_t c = c0 + i;
     const Chunk ck = chunks[c];
