@@ -340,9 +340,17 @@ constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 constexpr int32_t kAutoOther = DL_TUNE_NT_LOADS;
 // int8 encoder: its one 16-B payload store per lane non-temporal (tools/q8_layout.hip)
 constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
+// Launches over more than 2^28 elements (1 GiB of fp32, four times the Infinity Cache): their
+// output cannot stay cached for the next kernel, so the kernels that store plainly at bucket
+// size (dl_delta_pack, dl_gather; dl_scatter and dl_unpack_avg also take two chunks per
+// workgroup there) store non-temporally -- cold over a whole T1.3B tree dl_delta_pack 3 %,
+// dl_gather 1 %, dl_scatter / dl_unpack_avg 7 % faster; at T125 / bucket size the same policy
+// is 2-8 % slower (tools/cold_sweep.py "auto", profiles/r02_cold_sweep_flags_auto_*.json).
+constexpr int32_t kBigLaunchChunks = (1 << 28) / DL_CHUNK_ELEMS;
+enum class Big { keep, nt_stores, nt_stores_2 };
 
 int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who,
-                int32_t auto_flags = kAutoOther) {
+                int32_t auto_flags = kAutoOther, Big big = Big::keep) {
   if (!t) return fail(DL_E_ARG, "%s: null tree", who);
   const int32_t nb = int32_t(t->bounds.size()) - 1;
   if (b == DL_ALL_BUCKETS) {
@@ -359,6 +367,10 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
   L->nchunk = int32_t(t->chunks.size());
   L->grid = t->grid;
   L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
+  if (t->flags == DL_TUNE_AUTO && big != Big::keep && L->c1 - L->c0 >= kBigLaunchChunks) {
+    L->flags |= DL_TUNE_NT_STORES;
+    if (big == Big::nt_stores_2 && L->grid == 0) L->grid = (L->c1 - L->c0 + 1) / 2;
+  }
   L->stream = static_cast<hipStream_t>(s);
   L->slot_period = t->slot_period;
   L->slot_read = t->slot_read;
@@ -396,7 +408,7 @@ extern "C" {
 DL_API int dl_delta_pack(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,
                          void* wire, int32_t wire_dtype, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack", kAutoDelta));
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack", kAutoDelta, Big::nt_stores));
   DL_TRY(check_slot(t, inner_slot, "dl_delta_pack"));
   DL_TRY(check_packed(outer, "dl_delta_pack", "outer"));
   DL_TRY(check_packed(wire, "dl_delta_pack", "wire"));
@@ -408,7 +420,7 @@ DL_API int dl_delta_pack(dl_tree_t t, int32_t b, int32_t inner_slot, const float
 DL_API int dl_unpack_avg(dl_tree_t t, int32_t b, const void* wire, int32_t wire_dtype,
                          int32_t divisor, int32_t dst_slot, float* dst_packed, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_avg"));
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_avg", kAutoOther, Big::nt_stores_2));
   DL_TRY(check_packed(wire, "dl_unpack_avg", "wire"));
   DL_TRY(check_dtype(wire_dtype, "dl_unpack_avg"));
   if (divisor < 1) return fail(DL_E_ARG, "dl_unpack_avg: divisor %d", divisor);
@@ -730,7 +742,7 @@ DL_API int dl_unpack_sgd_q8(dl_tree_t t, int32_t b, const void* slots, float* ou
 DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int32_t dtype,
                      dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_gather"));
+  DL_TRY(make_launch(t, b, s, &L, "dl_gather", kAutoOther, Big::nt_stores));
   DL_TRY(check_slot(t, src_slot, "dl_gather"));
   DL_TRY(check_packed(packed, "dl_gather", "packed"));
   DL_TRY(check_dtype(dtype, "dl_gather"));
@@ -741,7 +753,7 @@ DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int
 DL_API int dl_scatter(dl_tree_t t, int32_t b, const float* packed, int32_t dst_slot,
                       dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_scatter"));
+  DL_TRY(make_launch(t, b, s, &L, "dl_scatter", kAutoOther, Big::nt_stores_2));
   DL_TRY(check_slot(t, dst_slot, "dl_scatter"));
   DL_TRY(check_packed(packed, "dl_scatter", "packed"));
   hipError_t e = dl::launch_scatter(L, packed, dst_slot);

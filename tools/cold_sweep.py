@@ -88,7 +88,7 @@ def main():
         # (flags, grid): grid half = two chunks per workgroup (grid-stride walk)
         flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (0, 0): "plain",
                       (2, 0): "nt_stores", (1, half): "nt_loads,2chunks/wg",
-                      (3, half): "nt_loads+stores,2chunks/wg"}
+                      (3, half): "nt_loads+stores,2chunks/wg", (_lib.TUNE_AUTO, 0): "auto"}
         res = {(k, f): [] for k in kern for f in flag_names}
         for _ in range(a.rounds):
             for (k, f) in res:
