@@ -76,3 +76,30 @@ def test_cpu_baseline_with_two_gloo_processes():
         r = json.load(f)
     assert r["cores"] == 2 and r["kind"] == "port" and r["value"] > 0
     assert "2 CPU processes" in r["sample"]
+
+
+def test_mix_ceiling_reads_each_half_against_its_own_probe():
+    """bench.with_copy_ceiling: a kernel of R bytes read from s_r buffers and W written to s_w
+    is held to t >= R / read_GBs[s_r] + W / write_GBs[s_w]; entries without a byte mix, or a
+    failed ceiling leg, pass through unchanged."""
+    import sys as _sys
+
+    _sys.path.insert(0, REPO)
+    import bench
+
+    ceiling = {"GBs": 6000.0, "read_GBs": {1: 6800.0, 2: 6900.0, 3: 7000.0, 4: 7000.0},
+               "write_GBs": {1: 6000.0, 2: 5800.0, 3: 5600.0, 4: 5500.0}}
+    # dl_delta_pack_sgd on T125: 12 B/param read from 3 streams, 16 B/param written to 4
+    P = 124_475_904
+    e = bench.kernel_entry(28 * P, 0.6, rw=(12 * P, 3, 16 * P, 4))
+    got = bench.with_copy_ceiling(e, ceiling)
+    t = 12 * P / 7000e9 + 16 * P / 5500e9
+    assert abs(got["mix_ceiling"] - 28 * P / t / 1e9) < 0.1
+    assert abs(got["frac_vs_mix"] - e["achieved"] / (28 * P / t / 1e9)) < 1e-3
+    assert got["frac_vs_copy"] == round(e["achieved"] / 6000.0, 4)
+    # a kernel that only reads (W = 0) is held to the read probe alone
+    r = bench.with_copy_ceiling(bench.kernel_entry(8 * P, 0.2, rw=(8 * P, 2, 0, 1)), ceiling)
+    assert r["mix_ceiling"] == 6900.0
+    plain = bench.kernel_entry(8 * P, 0.2)
+    assert "mix_ceiling" not in bench.with_copy_ceiling(plain, ceiling)
+    assert bench.with_copy_ceiling(e, {"ok": False, "error": "x"}) == e
