@@ -72,8 +72,9 @@ class SendThread:
         if serialize:
             self.serializer = Serializer(shape)
             self.shape = self.serializer.shape
+        self.thread = threading.Thread(target=self._send_loop, daemon=True) if start else None
         if start:
-            threading.Thread(target=self._send_loop, daemon=True).start()
+            self.thread.start()
 
     def send(self, dst: int, tensor: torch.Tensor, metadata: Optional[Metadata]) -> None:
         check_alive(self)
@@ -108,8 +109,9 @@ class RecvThread:
         if serialize:
             self.serializer = Serializer(shape)
             self.shape = self.serializer.shape
+        self.thread = threading.Thread(target=self._recv_loop, daemon=True) if start else None
         if start:
-            threading.Thread(target=self._recv_loop, daemon=True).start()
+            self.thread.start()
 
     @property
     def can_receive(self) -> bool:

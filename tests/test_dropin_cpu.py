@@ -57,6 +57,7 @@ def test_send_thread_failure_is_raised_to_the_caller():
     with pytest.raises(ThreadStopped) as e:
         t.send(0, torch.ones(4), (0, 0))
     assert isinstance(e.value.__cause__, IndexError)
+    t.thread.join(10)  # its excepthook warning lands in this test, not a later one
 
 
 @quiet_thread
@@ -65,6 +66,7 @@ def test_recv_thread_failure_wakes_a_blocked_receive():
     t = RecvThread((2, 2), group=None)
     with pytest.raises(ThreadStopped):
         t.receive()
+    t.thread.join(10)
     assert t.can_receive  # a training loop polling can_receive gets to the raise too
     with pytest.raises(ThreadStopped):
         t.receive()
