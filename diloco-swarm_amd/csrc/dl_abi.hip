@@ -267,7 +267,7 @@ DL_API int dl_tree_bucket_chunks(dl_tree_t t, int32_t b, int32_t* c0, int32_t* c
 DL_API int dl_tree_tune(dl_tree_t t, int32_t max_blocks, int32_t flags) {
   if (!t || max_blocks < 0) return fail(DL_E_ARG, "dl_tree_tune: bad argument");
   if (flags != DL_TUNE_AUTO &&
-      (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES | DL_TUNE_REVERSE)))
+      (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES | DL_TUNE_WT_STORES | DL_TUNE_REVERSE)))
     return fail(DL_E_ARG, "dl_tree_tune: unknown flags 0x%x", flags);
   t->grid = max_blocks;
   t->flags = flags;

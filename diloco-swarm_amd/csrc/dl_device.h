@@ -48,12 +48,29 @@ __device__ __forceinline__ float4 ldf4(const float* p, int v) {
   else r = *q;
   return make_float4(r.x, r.y, r.z, r.w);
 }
-template <bool NT>
+// Store policies (the walker's NTS template argument, dl_tree_tune's flags): plain, `nt`
+// (non-temporal), or write-through (`sc1`: the line leaves the XCD's L2 at once instead of
+// staying there dirty until evicted; tools/store_policy.hip). A write-through store goes
+// through a buffer descriptor of the stream's base, which is wave-uniform in every caller (a
+// chunk's stream base from the chunk table), so the descriptor lives in SGPRs; v < 2^27.
+enum : int { kStPlain = 0, kStNT = 1, kStWT = 2 };
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+constexpr int kAuxSc1 = 16;  // buffer-op cache policy bits, gfx950: sc0 = 1, nt = 2, sc1 = 16
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7fffffff, 0x00020000);
+}
+template <int SP>
 __device__ __forceinline__ void stf4(float* p, int v, float4 x) {
-  gf4 q = (gf4)(p) + v;
   const f32x4 r = {x.x, x.y, x.z, x.w};
-  if constexpr (NT) __builtin_nontemporal_store(r, q);
-  else *q = r;
+  if constexpr (SP == kStWT) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), stream_rsrc(p), v * 16, 0,
+                                           kAuxSc1);
+  } else {
+    gf4 q = (gf4)(p) + v;
+    if constexpr (SP == kStNT) __builtin_nontemporal_store(r, q);
+    else *q = r;
+  }
 }
 template <bool NT>
 __device__ __forceinline__ uint64_t ld8(const void* p, int v) {
@@ -61,11 +78,16 @@ __device__ __forceinline__ uint64_t ld8(const void* p, int v) {
   if constexpr (NT) return __builtin_nontemporal_load(q);
   else return *q;
 }
-template <bool NT>
+template <int SP>
 __device__ __forceinline__ void st8(void* p, int v, uint64_t x) {
-  gu64 q = (gu64)(p) + v;
-  if constexpr (NT) __builtin_nontemporal_store(x, q);
-  else *q = x;
+  if constexpr (SP == kStWT) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), stream_rsrc(p), v * 8, 0,
+                                          kAuxSc1);
+  } else {
+    gu64 q = (gu64)(p) + v;
+    if constexpr (SP == kStNT) __builtin_nontemporal_store(x, q);
+    else *q = x;
+  }
 }
 
 template <typename W>
@@ -75,8 +97,8 @@ template <>
 struct WireIO<float> {
   template <bool NT>
   static __device__ __forceinline__ float4 ld4(const float* p, int v) { return ldf4<NT>(p, v); }
-  template <bool NT>
-  static __device__ __forceinline__ void st4(float* p, int v, float4 x) { stf4<NT>(p, v, x); }
+  template <int SP>
+  static __device__ __forceinline__ void st4(float* p, int v, float4 x) { stf4<SP>(p, v, x); }
   static __device__ __forceinline__ float ld1(const float* p, int i) { return p[i]; }
   static __device__ __forceinline__ void st1(float* p, int i, float x) { p[i] = x; }
 };
@@ -89,11 +111,11 @@ struct WireIO<bf16_t> {
     return make_float4(bf2f(uint16_t(r)), bf2f(uint16_t(r >> 16)), bf2f(uint16_t(r >> 32)),
                        bf2f(uint16_t(r >> 48)));
   }
-  template <bool NT>
+  template <int SP>
   static __device__ __forceinline__ void st4(bf16_t* p, int v, float4 x) {
     const uint64_t r = uint64_t(f2bf(x.x)) | (uint64_t(f2bf(x.y)) << 16) |
                        (uint64_t(f2bf(x.z)) << 32) | (uint64_t(f2bf(x.w)) << 48);
-    st8<NT>(p, v, r);
+    st8<SP>(p, v, r);
   }
   static __device__ __forceinline__ float ld1(const bf16_t* p, int i) { return bf2f(p[i].bits); }
   static __device__ __forceinline__ void st1(bf16_t* p, int i, float x) { p[i].bits = f2bf(x); }
@@ -112,7 +134,7 @@ __device__ __forceinline__ float4 div4(float4 a, float d) {
 // the 7-stream shape gained 4 % from it (tools/mem_ceiling.hip dps_o); in the product kernels
 // the cold A/B against the row-by-row order is neutral within noise (tools/gpu_ab_cold.sh,
 // profiles/r02_ab_store_order.txt). Rows past the chunk (v >= nv) hold no data and are skipped.
-template <bool NTS>
+template <int NTS>
 __device__ __forceinline__ void store_rows(float* p, const float4 (&x)[kUnroll], int nv, int tid) {
 #pragma unroll
   for (int u = 0; u < kUnroll; ++u) {
@@ -127,11 +149,11 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 }
 
 // ---- the walker ----------------------------------------------------------------------------
-// Body::operator() is instantiated per (NTL, NTS) policy: non-temporal loads / stores.
+// Body::run is instantiated per (NTL, NTS) policy: non-temporal loads; plain / NT / WT stores.
 // rev: walk the range last chunk first (workgroups are dispatched in blockIdx order), so a
 // kernel that follows one which streamed the same buffers front to back starts on the bytes
 // most likely still in the Infinity Cache.
-template <class Body, bool NTL, bool NTS>
+template <class Body, bool NTL, int NTS>
 __global__ void __launch_bounds__(kThreads)
     k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ caddr,
            int32_t nchunk, int32_t rev, Body body) {
@@ -182,7 +204,7 @@ struct SlotGate {
   }
 };
 
-template <class Body, bool NTL, bool NTS>
+template <class Body, bool NTL, int NTS>
 __global__ void __launch_bounds__(kThreads)
     k_walk_slotted(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1,
                    void* const* __restrict__ caddr, int32_t nchunk, uint32_t period,
@@ -216,7 +238,7 @@ struct slotted : std::false_type {};
 template <class B>
 struct slotted<B, std::void_t<decltype(B::kSlotted)>> : std::bool_constant<B::kSlotted> {};
 
-template <class Body, bool NTL, bool NTS>
+template <class Body, bool NTL, int NTS>
 hipError_t run_policy(const Launch& L, const Body& body, int32_t grid) {
   if constexpr (slotted<Body>::value) {
     if (L.slot_period > 0) {
@@ -239,11 +261,16 @@ hipError_t run(const Launch& L, const Body& body) {
   const int32_t n = L.c1 - L.c0;
   if (n <= 0) return hipSuccess;
   const int32_t grid = (L.grid > 0 && L.grid < n) ? L.grid : n;  // default: one workgroup per chunk
-  const bool ntl = (L.flags & DL_TUNE_NT_LOADS) != 0, nts = (L.flags & DL_TUNE_NT_STORES) != 0;
-  if (ntl && nts) return run_policy<Body, true, true>(L, body, grid);
-  if (ntl) return run_policy<Body, true, false>(L, body, grid);
-  if (nts) return run_policy<Body, false, true>(L, body, grid);
-  return run_policy<Body, false, false>(L, body, grid);
+  const bool ntl = (L.flags & DL_TUNE_NT_LOADS) != 0;
+  const int sp = (L.flags & DL_TUNE_WT_STORES) ? kStWT : (L.flags & DL_TUNE_NT_STORES) ? kStNT : kStPlain;
+  if (ntl) {
+    if (sp == kStWT) return run_policy<Body, true, kStWT>(L, body, grid);
+    if (sp == kStNT) return run_policy<Body, true, kStNT>(L, body, grid);
+    return run_policy<Body, true, kStPlain>(L, body, grid);
+  }
+  if (sp == kStWT) return run_policy<Body, false, kStWT>(L, body, grid);
+  if (sp == kStNT) return run_policy<Body, false, kStNT>(L, body, grid);
+  return run_policy<Body, false, kStPlain>(L, body, grid);
 }
 
 }  // namespace

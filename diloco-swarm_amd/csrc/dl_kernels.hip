@@ -29,7 +29,7 @@ struct DeltaPack {
   const float* outer;
   W* wire;
   static constexpr bool kSlotted = true;
-  template <bool NTL, bool NTS, class G = NoGate>
+  template <bool NTL, int NTS, class G = NoGate>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
                                       const G& gate = G()) const {
     const float* in = slot_ptr<const float>(caddr, nchunk, inner_slot, c);
@@ -68,7 +68,7 @@ struct UnpackAvg {
   int dst_slot;
   float* dst_packed;
   float d;
-  template <bool NTL, bool NTS>
+  template <bool NTL, int NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* dst = dst_slot >= 0 ? slot_ptr<float>(caddr, nchunk, dst_slot, c) : dst_packed + ck.poff;
     const W* w = wire + ck.poff;
@@ -108,7 +108,7 @@ struct UnpackSgd {
   SgdArgs a;
   int inner_slot;
   static constexpr bool kSlotted = true;
-  template <bool NTL, bool NTS, class G = NoGate>
+  template <bool NTL, int NTS, class G = NoGate>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
                                       const G& gate = G()) const {
     float* in = inner_slot >= 0 ? slot_ptr<float>(caddr, nchunk, inner_slot, c) : nullptr;
@@ -174,7 +174,7 @@ struct DeltaSgd {
   SgdArgs a;
   int inner_slot;
   static constexpr bool kSlotted = true;
-  template <bool NTL, bool NTS, class G = NoGate>
+  template <bool NTL, int NTS, class G = NoGate>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
                                       const G& gate = G()) const {
     float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
@@ -245,7 +245,7 @@ struct DeltaPackSgd {
     else return g;
   }
   static constexpr bool kSlotted = true;
-  template <bool NTL, bool NTS, class G = NoGate>
+  template <bool NTL, int NTS, class G = NoGate>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
                                       const G& gate = G()) const {
     float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
@@ -315,7 +315,7 @@ template <typename W>
 struct Gather {
   int src_slot;
   W* packed;
-  template <bool NTL, bool NTS>
+  template <bool NTL, int NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     const float* src = slot_ptr<const float>(caddr, nchunk, src_slot, c);
     W* p = packed + ck.poff;
@@ -344,7 +344,7 @@ struct Gather {
 struct Scatter {
   const float* packed;
   int dst_slot;
-  template <bool NTL, bool NTS>
+  template <bool NTL, int NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* dst = slot_ptr<float>(caddr, nchunk, dst_slot, c);
     const float* p = packed + ck.poff;

@@ -64,7 +64,7 @@ struct DeltaQ8 {
   const float* outer;
   uint8_t* slots;  // slot of chunk c at (c - c0) * DL_Q8_SLOT_BYTES
   int c0;
-  template <bool NTL, bool NTS>
+  template <bool NTL, int NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     __shared__ u32x4 stage[DL_CHUNK_ELEMS / 16];  // the payload, 16 B per lane
     uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
@@ -142,7 +142,7 @@ struct UnpackSgdQ8 {
   float* mom;
   SgdArgs a;
   int inner_slot;
-  template <bool NTL, bool NTS>
+  template <bool NTL, int NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* in = inner_slot >= 0 ? slot_ptr<float>(caddr, nchunk, inner_slot, c) : nullptr;
     const uint8_t* slot = slots + size_t(c - c0) * DL_Q8_SLOT_BYTES;

@@ -101,13 +101,15 @@ DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, 
                         dl_stream_t stream);
 /* Launch shape of every walker kernel on this tree: max_blocks caps the grid (0 = one
  * workgroup per chunk, the default); flags = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES |
- * DL_TUNE_REVERSE selects non-temporal loads / stores / a last-to-first chunk order for every
- * kernel, DL_TUNE_AUTO (the default) the measured
+ * DL_TUNE_WT_STORES | DL_TUNE_REVERSE selects non-temporal loads / non-temporal stores /
+ * write-through stores (sc1; wins over NT_STORES; the int8 encoder's payload stays NT) / a
+ * last-to-first chunk order for every kernel, DL_TUNE_AUTO (the default) the measured
  * per-kernel choice (NT loads everywhere, NT stores in dl_unpack_sgd). Results are
  * identical for every setting; only speed differs. */
 #define DL_TUNE_NT_LOADS 1
 #define DL_TUNE_NT_STORES 2
 #define DL_TUNE_REVERSE 4 /* walk chunks last to first */
+#define DL_TUNE_WT_STORES 8 /* write-through (sc1) stores */
 #define DL_TUNE_AUTO (-1)
 DL_API int dl_tree_tune(dl_tree_t tree, int32_t max_blocks, int32_t flags);
 

@@ -37,6 +37,9 @@ def test_header_constants_match_python_mirror():
     src = open(HEADER).read()
     consts = dict(re.findall(r"#define (DL_\w+) \(?(-?\d+)\)?", src))
     assert int(consts["DL_TUNE_AUTO"]) == _lib.TUNE_AUTO
+    assert (int(consts["DL_TUNE_NT_LOADS"]), int(consts["DL_TUNE_NT_STORES"]),
+            int(consts["DL_TUNE_REVERSE"]), int(consts["DL_TUNE_WT_STORES"])) == (
+        _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_REVERSE, _lib.TUNE_WT_STORES)
     assert (int(consts["DL_COPY_WIDE"]), int(consts["DL_COPY_READ"]),
             int(consts["DL_COPY_WRITE"])) == (_lib.COPY_WIDE, _lib.COPY_READ, _lib.COPY_WRITE)
     assert int(consts["DL_ALIGN_ELEMS"]) == _lib.ALIGN_ELEMS

@@ -391,6 +391,64 @@ def test_slotted_launches_are_bit_identical(kernel, period, read, misaligned):
     eb.close()
 
 
+@pytest.mark.parametrize("kernel", ["delta_pack_sgd", "delta_pack_sgd_bf16", "delta_sgd",
+                                    "two_kernel", "two_kernel_bf16"])
+@pytest.mark.parametrize("misaligned", [False, True])
+def test_store_policies_are_bit_identical(kernel, misaligned):
+    """dl_tree_tune's store policies (plain, non-temporal, write-through sc1 buffer stores, both
+    flags) change only the timing: θ, momentum, the wire (fp32 and bf16) and the inner params
+    equal the AUTO policy's bit for bit, ragged tails and the 4-B-aligned scalar path included."""
+    sizes = RAGGED + [300 * 4096 + 77]
+    g0 = torch.Generator().manual_seed(37)
+    host = [torch.randn(n, generator=g0) for n in sizes]
+
+    def place():
+        if not misaligned:
+            return [h.to(DEV) for h in host]
+        base = torch.empty(sum(sizes) + len(sizes), device=DEV)
+        out, o = [], 1
+        for h in host:
+            out.append(base[o:o + h.numel()])
+            out[-1].copy_(h)
+            o += h.numel() + 1
+        return out
+
+    wire = torch.bfloat16 if kernel.endswith("bf16") else torch.float32
+    kw = {"delta_pack_sgd": dict(fuse_single=True, keep_wire=True, wire_dtype=wire),
+          "delta_sgd": dict(fuse_single=True),
+          "two_kernel": dict(fuse_single=False, tile_chunks=0, wire_dtype=wire)}[
+              kernel.replace("_bf16", "")]
+    NTL, NTS, WT = _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_WT_STORES
+    policies = [NTL, NTL | NTS, NTL | WT, NTL | NTS | WT, WT]
+    ref_p = place()
+    ref = OuterSync(ref_p, world_size=1, **kw)
+    runs = []
+    for f in policies:
+        p = place()
+        e = OuterSync(p, world_size=1, **kw)
+        e.tree.tune(0, f)
+        runs.append((e, p))
+    for _ in range(2):
+        noise = [torch.randn(n, generator=g0).to(DEV) * 1e-3 for n in sizes]
+        for ps in [ref_p] + [p for _, p in runs]:
+            for t, z in zip(ps, noise):
+                t.add_(z)
+        ref.step()
+        for e, _ in runs:
+            e.step()
+        torch.cuda.synchronize()
+        for e, p in runs:
+            assert torch.equal(e.theta.view(torch.int32), ref.theta.view(torch.int32))
+            assert torch.equal(e.mom.view(torch.int32), ref.mom.view(torch.int32))
+            if ref.wire is not None and kernel != "delta_sgd":
+                assert torch.equal(e.wire.view(torch.uint8), ref.wire.view(torch.uint8))
+            for a, b in zip(p, ref_p):
+                assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    for e, _ in runs:
+        e.close()
+    ref.close()
+
+
 def test_delta_pack_sgd_micro_matches_reference():
     """The one-pass step with the wire kept reproduces the reference's outer steps AND its
     outer.grad (the wire holds delta_s{s}_r0 after step s), micro tree, n = 1."""

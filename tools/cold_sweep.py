@@ -6,7 +6,7 @@ every timed launch, variants interleaved round by round in one process (cdna_hip
 
     python tools/cold_sweep.py [--tree t125] [--rounds 11] [--out x.json] [--what flags,tiles]
 
-flags : dl_tree_tune launch policy (NT loads / NT stores) of dl_delta_pack, dl_unpack_sgd,
+flags : dl_tree_tune launch policy (NT loads / NT or write-through stores) of dl_delta_pack, dl_unpack_sgd,
         dl_delta_sgd one launch over the whole tree each
 tiles : the one-replica two-kernel step (dl_pack_sgd_tiled) at tile sizes 0 (whole-range
         launches), 1024 ... 16384 chunks, against the one-pass dl_delta_sgd
@@ -88,7 +88,8 @@ def main():
         # (flags, grid): grid half = two chunks per workgroup (grid-stride walk)
         flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (0, 0): "plain",
                       (2, 0): "nt_stores", (1, half): "nt_loads,2chunks/wg",
-                      (3, half): "nt_loads+stores,2chunks/wg", (_lib.TUNE_AUTO, 0): "auto"}
+                      (3, half): "nt_loads+stores,2chunks/wg", (_lib.TUNE_AUTO, 0): "auto",
+                      (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores"}
         res = {(k, f): [] for k in kern for f in flag_names}
         for _ in range(a.rounds):
             for (k, f) in res:
@@ -124,7 +125,8 @@ def main():
         kern = {"delta_q8": (lambda: e.pseudo_gradient(0), 8 * P + slot_bytes),
                 "q8_reduce": (red, 2 * slot_bytes),
                 "unpack_sgd_q8": (unpack, slot_bytes + 20 * P)}
-        shapes = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (1, half): "nt_loads,2chunks/wg"}
+        shapes = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (1, half): "nt_loads,2chunks/wg",
+                  (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores"}
         res = {(k, f): [] for k in kern for f in shapes}
         for _ in range(a.rounds):
             for (k, f) in res:

@@ -38,6 +38,7 @@ constexpr int T = 256;
 constexpr int U = 4;  // float4 per lane per stream: one workgroup = 4096 elements, as the walker
 constexpr int kTileBytes = U * T * 16;
 
+// the workgroup's first float4 (one workgroup = U * T float4 = 4096 elements)
 __device__ __forceinline__ long tile_base() { return long(blockIdx.x) * (U * T); }
 
 __device__ __forceinline__ f4 ldnt(const float* p, long v) {
@@ -46,7 +47,7 @@ __device__ __forceinline__ f4 ldnt(const float* p, long v) {
 
 // the workgroup's tile of one stream as a buffer resource (wave-uniform inputs only)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(p + tile_base(), 0, kTileBytes, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(p + 4 * tile_base(), 0, kTileBytes, 0x00020000);
 }
 
 template <int AUX>
@@ -127,7 +128,7 @@ __global__ void fill(float* p, long n, unsigned seed) {
 
 __global__ void check_k(const float* p, long n, unsigned* bad) {
   for (long i = blockIdx.x * long(T) + threadIdx.x; i < n; i += long(gridDim.x) * T) {
-    const float f = float(i) * 1e-9f;  // stream 0 of writeS
+    const float f = float(i >> 2) * 1e-9f;  // stream 0 of writeS (one value per float4)
     if (p[i] != f) atomicAdd(bad, 1u);
   }
 }
