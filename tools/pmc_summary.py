@@ -10,6 +10,7 @@ Counters are summed over the dimensions rocprofv3 reports per dispatch, then ave
 dispatches of each kernel.
 """
 import csv
+import re
 import json
 import sys
 from collections import defaultdict
@@ -27,10 +28,12 @@ def short(name):
         return "xgmi_delta_sgd"  # the pack-free variant (exchange="xgmi_inner")
     for k, v in names.items():
         if k in name:
-            first = ((k in ("UnpackSgd", "k_flat") and ", 1>" in name)
-                     or (k == "DeltaSgd" and "DeltaSgd<1>" in name)
-                     or (k == "DeltaPackSgd" and ", 1>" in name)
-                     or (k == "UnpackSgdQ8" and "UnpackSgdQ8<1>" in name))
+            # the SGD bodies' MODE (1 = first step) is the last argument of the body's own
+            # template list (k_walk's trailing arguments are the load / store policy)
+            body = "UnpackSgd" if k == "k_flat" else k
+            m = re.search(re.escape(body) + r"<([^<>]*)>", name)
+            first = (k in ("UnpackSgd", "k_flat", "DeltaSgd", "DeltaPackSgd", "UnpackSgdQ8")
+                     and m is not None and m.group(1).split(",")[-1].strip() == "1")
             return v + ("_first" if first else "")
     return None
 

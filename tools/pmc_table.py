@@ -24,8 +24,8 @@ def load(paths):
     for path in paths:
         for r in csv.DictReader(open(path)):
             name = r["Kernel_Name"]
-            k = short(name) or ("copy" if "k_copy<true>" in name else
-                                "scrub" if "k_copy<false>" in name else None)
+            k = short(name) or ("copy" if "k_copy<true" in name else
+                                "scrub" if "k_copy<false" in name else None)
             if k is None:
                 continue
             per[(k, path + r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
