@@ -106,6 +106,35 @@ def main():
                   f"  best {s['best_GBs']:7.1f}", flush=True)
         for e in (two, one, kept):
             e.close()
+    if "grids" in what:
+        # resident-grid caps (dl_tree_tune max_blocks, grid-stride walk): k workgroups per CU
+        # instead of one workgroup per chunk (tools/occupancy.hip: the memory system saturates
+        # with very few waves), AUTO policy, the one-pass kept-wire step and the SGD unpack
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True)
+        two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
+        for e in (kept, two):
+            e.step()
+        kern = {"delta_pack_sgd": (kept, lambda: kept._step(None), 28),
+                "unpack_sgd": (two, two.apply, 24), "delta_pack": (two, two.pseudo_gradient, 12)}
+        grids = {0: "one WG per chunk"}
+        grids.update({k * cus: f"{k} WG/CU resident" for k in (1, 2, 3, 4, 6)})
+        res = {(k, g): [] for k in kern for g in grids}
+        for _ in range(a.rounds):
+            for (k, g) in res:
+                eng, fn, _ = kern[k]
+                eng.tree.tune(g, _lib.TUNE_AUTO)
+                res[(k, g)].append(timed_cold(fn, scrub))
+        for e in (kept, two):
+            e.tree.tune(0, _lib.TUNE_AUTO)
+        out["grids"] = {}
+        for (k, g), ms in res.items():
+            s = summarize(ms, kern[k][2] * P)
+            out["grids"].setdefault(k, {})[grids[g]] = s
+            print(f"{k:14s} {grids[g]:26s} med {s['med_ms']:.4f} ms {s['med_GBs']:7.1f} GB/s"
+                  f"  best {s['best_GBs']:7.1f}", flush=True)
+        for e in (kept, two):
+            e.close()
     if "q8" in what:  # the int8 wire's kernels, one bucket (every launch covers the tree)
         from diloco_amd.kernels import Q8_SLOT
 
