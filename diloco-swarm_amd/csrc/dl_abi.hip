@@ -538,6 +538,25 @@ DL_API int dl_shard_sgd(const void* wire, int32_t wire_dtype, int32_t divisor, f
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_shard_sgd");
 }
 
+DL_API int dl_shard_reduce_sgd(const void* slices, int32_t wire_dtype, int32_t n_slices,
+                               int64_t len, float* outer, float* mom, float lr, float momentum,
+                               int32_t nesterov, int32_t first_step, dl_stream_t s) {
+  if (len < 0 || len % 4 != 0)
+    return fail(DL_E_ARG, "dl_shard_reduce_sgd: len %lld (a multiple of 4)", (long long)len);
+  if (n_slices < 1) return fail(DL_E_ARG, "dl_shard_reduce_sgd: n_slices %d", n_slices);
+  if (len == 0) return DL_OK;
+  DL_TRY(check_packed(slices, "dl_shard_reduce_sgd", "slices"));
+  DL_TRY(check_dtype(wire_dtype, "dl_shard_reduce_sgd"));
+  DL_TRY(check_packed(outer, "dl_shard_reduce_sgd", "outer"));
+  if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_shard_reduce_sgd", "momentum"));
+  if (nesterov && momentum == 0.f)
+    return fail(DL_E_ARG, "dl_shard_reduce_sgd: Nesterov momentum requires a momentum");
+  dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  hipError_t e = dl::launch_slices_sgd(slices, wire_dtype, n_slices, len, outer, mom, a,
+                                       static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_shard_reduce_sgd");
+}
+
 DL_API int dl_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
   if (!ptr || !handle || !offset) return fail(DL_E_ARG, "dl_ipc_handle: null argument");
   void* base = nullptr;

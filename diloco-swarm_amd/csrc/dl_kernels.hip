@@ -665,6 +665,114 @@ hipError_t launch_shard_sgd(const void* wire, int wire_dtype, int divisor, float
   return shard_sgd_t(static_cast<const float*>(wire), divisor, outer, mom, n, a, s);
 }
 
+// a3 + a4 after an all_to_all (OuterSync(exchange="a2a"), the deterministic alternative to a
+// SUM reduce-scatter): `slices` holds n equal slices of `len` elements of wire type W, slice q
+// being rank q's copy of this peer's shard. g = ((s_0 + s_1) + ... + s_{n-1}) / n in fp32, in
+// rank order -- the order of oracle/or_sum_avg and dl_xgmi_reduce_sgd, identical on every
+// rank whatever the transport -- then dl_shard_sgd's SGD on this peer's θ and momentum shards.
+// Reads n·sizeof(W) + 8 B, writes 8 B per shard element. N = 0: n read at run time (n > 8).
+constexpr int kSU = 2;                          // float4 rows per lane
+constexpr int64_t kSliceStep = kThreads * kSU * 4;  // 2048 elements per workgroup and round
+template <int N, typename W, int MODE>
+__global__ void __launch_bounds__(kThreads)
+    k_slices_sgd(const W* __restrict__ slices, int32_t n, int64_t len, float* __restrict__ th,
+                 float* __restrict__ mom, SgdArgs a) {
+  const int nn = N > 0 ? N : n;
+  for (int64_t base = int64_t(blockIdx.x) * kSliceStep; base < len;
+       base += int64_t(gridDim.x) * kSliceStep) {
+    const int32_t nv = int32_t((len - base) / 4 < kThreads * kSU ? (len - base) / 4 : kThreads * kSU);
+    float* t0 = th + base;
+    float* m0 = mom + base;
+    float4 g[kSU], t[kSU], m[kSU];
+    if constexpr (N > 0) {
+      float4 w[N][kSU];
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        const int v = u * kThreads + int(threadIdx.x);
+        if (v < nv) {
+#pragma unroll
+          for (int q = 0; q < N; ++q) w[q][u] = WireIO<W>::template ld4<true>(slices + q * len + base, v);
+          t[u] = ldf4<true>(t0, v);
+          if (MODE == 2) m[u] = ldf4<true>(m0, v);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        g[u] = w[0][u];
+#pragma unroll
+        for (int q = 1; q < N; ++q)
+          g[u] = make_float4(g[u].x + w[q][u].x, g[u].y + w[q][u].y, g[u].z + w[q][u].z,
+                             g[u].w + w[q][u].w);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        const int v = u * kThreads + int(threadIdx.x);
+        if (v < nv) {
+          t[u] = ldf4<true>(t0, v);
+          if (MODE == 2) m[u] = ldf4<true>(m0, v);
+          g[u] = WireIO<W>::template ld4<true>(slices + base, v);
+          for (int q = 1; q < nn; ++q) {
+            const float4 d = WireIO<W>::template ld4<true>(slices + q * len + base, v);
+            g[u] = make_float4(g[u].x + d.x, g[u].y + d.y, g[u].z + d.z, g[u].w + d.w);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      const int v = u * kThreads + int(threadIdx.x);
+      if (v < nv) {
+        const float4 gg = nn > 1 ? div4(g[u], float(nn)) : g[u];
+        sgd1<MODE>(gg.x, m[u].x, t[u].x, a);
+        sgd1<MODE>(gg.y, m[u].y, t[u].y, a);
+        sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
+        sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
+        stf4<kStNT>(t0, v, t[u]);
+        if (MODE != 0) stf4<kStNT>(m0, v, m[u]);
+      }
+    }
+  }
+}
+
+template <int N, typename W>
+static hipError_t slices_sgd_n(const W* w, int32_t n, int64_t len, float* th, float* mom,
+                               SgdArgs a, hipStream_t s) {
+  const int64_t blocks = (len + kSliceStep - 1) / kSliceStep;
+  const int32_t grid = int32_t(blocks < (1 << 20) ? blocks : (1 << 20));
+  if (a.momentum == 0.f)
+    hipLaunchKernelGGL((k_slices_sgd<N, W, 0>), dim3(grid), dim3(kThreads), 0, s, w, n, len, th, mom, a);
+  else if (a.first)
+    hipLaunchKernelGGL((k_slices_sgd<N, W, 1>), dim3(grid), dim3(kThreads), 0, s, w, n, len, th, mom, a);
+  else
+    hipLaunchKernelGGL((k_slices_sgd<N, W, 2>), dim3(grid), dim3(kThreads), 0, s, w, n, len, th, mom, a);
+  return hipGetLastError();
+}
+
+template <typename W>
+static hipError_t slices_sgd_t(const W* w, int32_t n, int64_t len, float* th, float* mom,
+                               SgdArgs a, hipStream_t s) {
+  switch (n) {
+    case 1: return slices_sgd_n<1>(w, n, len, th, mom, a, s);
+    case 2: return slices_sgd_n<2>(w, n, len, th, mom, a, s);
+    case 3: return slices_sgd_n<3>(w, n, len, th, mom, a, s);
+    case 4: return slices_sgd_n<4>(w, n, len, th, mom, a, s);
+    case 5: return slices_sgd_n<5>(w, n, len, th, mom, a, s);
+    case 6: return slices_sgd_n<6>(w, n, len, th, mom, a, s);
+    case 7: return slices_sgd_n<7>(w, n, len, th, mom, a, s);
+    case 8: return slices_sgd_n<8>(w, n, len, th, mom, a, s);
+    default: return slices_sgd_n<0>(w, n, len, th, mom, a, s);
+  }
+}
+
+hipError_t launch_slices_sgd(const void* slices, int wire_dtype, int32_t n, int64_t len,
+                             float* outer, float* mom, SgdArgs a, hipStream_t s) {
+  if (len <= 0) return hipSuccess;
+  if (wire_dtype == DL_BF16)
+    return slices_sgd_t(static_cast<const bf16_t*>(slices), n, len, outer, mom, a, s);
+  return slices_sgd_t(static_cast<const float*>(slices), n, len, outer, mom, a, s);
+}
+
 hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float* mom, SgdArgs a) {
   if (a.momentum == 0.f) return run(L, DeltaSgd<0>{outer, mom, a, inner_slot});
   if (a.first) return run(L, DeltaSgd<1>{outer, mom, a, inner_slot});

@@ -93,6 +93,14 @@ class HipKernels:
                   theta.data_ptr(), _ptr(mom), theta.numel(), float(lr), float(momentum),
                   int(nesterov), int(first), _s(theta))
 
+    def shard_reduce_sgd(self, slices, n_slices, theta, mom, lr, momentum, nesterov,
+                         first) -> None:
+        """Flat 1/n shard after an all_to_all: slices = n_slices equal slices (wire dtype) of
+        theta's length; Σ in rank order, /n, SGD on theta / mom (equal-length views)."""
+        _lib.call("dl_shard_reduce_sgd", slices.data_ptr(), wire_code(slices.dtype),
+                  int(n_slices), theta.numel(), theta.data_ptr(), _ptr(mom), float(lr),
+                  float(momentum), int(nesterov), int(first), _s(theta))
+
     def xgmi_reduce_sgd(self, wires, thetas, n, rank, lo, length, mom, lr, momentum, nesterov,
                         first, device=None) -> None:
         """Direct exchange on this rank's shard (wires / thetas: uint64 arrays of the n peers'

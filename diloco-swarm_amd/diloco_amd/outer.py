@@ -16,6 +16,10 @@ Exchange variants, all bucketed and pipelined across buckets:
   sharded            (default for n > 1 with the fp32 wire) RCCL reduce-scatter ->
                      dl_shard_sgd on this peer's 1/n (θ and momentum shards) -> RCCL all-gather
                      of θ -> dl_scatter; HBM 20 + 20/n B/param, momentum 4P/n
+  sharded, ordered   exchange="a2a": the reduce-scatter becomes an RCCL all_to_all of the wire
+                     slices + dl_shard_reduce_sgd (Σ in rank order in fp32, /n, SGD): the same
+                     bus bytes, a result that does not depend on RCCL's algorithm, bit-exact
+                     against the oracle at every n; a bf16 wire is summed in fp32
   replicated         (shard=False; the bf16 wire's default) RCCL all-reduce -> dl_unpack_sgd
                      (/n + SGD + copy-back, 24 B/param) on every replica
   int8 wire          dl_delta_q8 -> all_to_all -> dl_q8_reduce -> all_gather -> dl_unpack_sgd_q8
@@ -129,6 +133,7 @@ class OuterSync:
         if wire_dtype not in (torch.float32, torch.bfloat16, torch.int8):
             raise ValueError(f"wire dtype {wire_dtype}: float32, bfloat16 or int8")
         self.q8 = wire_dtype == torch.int8
+        shard_given = shard
         if shard is None:
             # fp32 wire: same bus bytes as the all-reduce, fewer HBM bytes. bf16 wire: the
             # fp32 all-gather of θ would move 6(n-1)/n B/param against the bf16 all-reduce's
@@ -136,8 +141,17 @@ class OuterSync:
             shard = self.world_size > 1 and wire_dtype == torch.float32
         if shard and self.q8:
             raise ValueError("the int8 wire has its own exchange; shard=True needs f32/bf16")
-        if exchange not in ("rccl", "xgmi", "xgmi_inner"):
-            raise ValueError(f"exchange {exchange!r}: 'rccl', 'xgmi' or 'xgmi_inner'")
+        if exchange not in ("rccl", "a2a", "xgmi", "xgmi_inner"):
+            raise ValueError(f"exchange {exchange!r}: 'rccl', 'a2a', 'xgmi' or 'xgmi_inner'")
+        # a2a: the sharded step with an all_to_all of the wire slices and a rank-order reduce
+        # (dl_shard_reduce_sgd) in place of the SUM reduce-scatter
+        self.a2a = exchange == "a2a"
+        if self.a2a:
+            if self.q8:
+                raise ValueError("exchange='a2a' exchanges the f32 or bf16 wire")
+            if shard_given is False:
+                raise ValueError("exchange='a2a' is a sharded step (shard=False contradicts it)")
+            shard = True
         # xgmi: the direct peer-access exchange (dl_xgmi_reduce_sgd) over IPC-mapped buffers
         # xgmi_inner: the same with no wire -- the inner parameters move into one packed arena
         # that the peers read, and the exchange kernel forms θ_outer - inner_q itself
@@ -190,9 +204,14 @@ class OuterSync:
             self.th_shard = torch.empty(off, dtype=torch.float32, **z)
             for b in range(self.tree.n_buckets):
                 self.th_shard_view(b).copy_(self.theta_shard_of(b))
-            self.g_shard = torch.zeros(off, dtype=wire_dtype, **z)
+            self.g_shard = None if self.a2a else torch.zeros(off, dtype=wire_dtype, **z)
             self.mom_shard = (torch.zeros(off, dtype=torch.float32, **z)
                               if self.momentum != 0 else None)
+            if self.a2a:
+                # all_to_all landing buffers, one per bucket in flight (the step overlaps the
+                # exchange of bucket b+1 with the reduce of bucket b): n slices of the shard
+                smax = max(self._shard_len(b) for b in range(self.tree.n_buckets))
+                self.a2a_recv = [torch.zeros(n * smax, dtype=wire_dtype, **z) for _ in range(2)]
         if self.xgmi:
             from .xgmi import PeerMap
 
@@ -310,8 +329,18 @@ class OuterSync:
             return False
         return not dist.is_initialized() or dist.get_world_size(self.group) != 1
 
+    def _a2a_slices(self, bucket: int) -> torch.Tensor:
+        return self.a2a_recv[bucket % 2][:self.world_size * self._shard_len(bucket)]
+
     def reduce_scatter(self, bucket: int, async_op: bool = True):
-        """SUM reduce-scatter of one wire bucket: this peer receives the sum of its 1/n."""
+        """SUM reduce-scatter of one wire bucket: this peer receives the sum of its 1/n.
+        exchange="a2a": an all_to_all instead -- this peer receives the n ranks' copies of its
+        1/n, summed in rank order by shard_apply."""
+        if self.a2a:
+            if self._local():  # one replica: the bucket itself is the one slice
+                return _Done()
+            return dist.all_to_all_single(self._a2a_slices(bucket), self.bucket_view(bucket),
+                                          group=self.group, async_op=async_op)
         if self._local():
             self._shard(self.g_shard, bucket).copy_(self.bucket_view(bucket))
             return _Done()
@@ -321,6 +350,12 @@ class OuterSync:
 
     def shard_apply(self, bucket: int) -> None:
         """g = Σ/n; Nesterov SGD on this peer's θ and momentum shards (a3 /n, a4)."""
+        if self.a2a:
+            slices = self.bucket_view(bucket) if self._local() else self._a2a_slices(bucket)
+            self.k.shard_reduce_sgd(slices, self.world_size, self.th_shard_view(bucket),
+                                    self._shard(self.mom_shard, bucket), self.lr, self.momentum,
+                                    self.nesterov, self.steps_done == 0)
+            return
         self.k.shard_sgd(self._shard(self.g_shard, bucket), self.world_size,
                          self.th_shard_view(bucket), self._shard(self.mom_shard, bucket),
                          self.lr, self.momentum, self.nesterov, self.steps_done == 0)

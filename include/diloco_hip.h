@@ -198,6 +198,18 @@ DL_API int dl_shard_sgd(const void* wire, int32_t wire_dtype, int32_t divisor, f
                         float* mom, int64_t n, float lr, float momentum, int32_t nesterov,
                         int32_t first_step, dl_stream_t stream);
 
+/* a3 (Σ, /n) + a4 on one peer's shard after an all_to_all instead of a reduce-scatter
+ * (OuterSync(exchange="a2a")): `slices` holds n_slices equal slices of `len` elements
+ * (wire dtype), slice q = rank q's copy of this peer's shard of the bucket
+ * (src/comm.py:122 `all_reduce(SUM)` + :123 `/= num_peers`, then the SGD of src/train.py:267).
+ * g = ((s_0 + s_1) + ... + s_{n-1}) / n in fp32 in rank order -- deterministic and identical
+ * on every rank, bit-exact against oracle/or_sum_avg at every n (a bf16 wire is summed in
+ * fp32 and never re-rounded) -- then dl_shard_sgd's SGD on outer[k], mom[k]. len a multiple
+ * of 4; all pointers 16-B aligned. Reads n·sizeof(wire) + 8 B, writes 8 B per element. */
+DL_API int dl_shard_reduce_sgd(const void* slices, int32_t wire_dtype, int32_t n_slices,
+                               int64_t len, float* outer, float* mom, float lr, float momentum,
+                               int32_t nesterov, int32_t first_step, dl_stream_t stream);
+
 /* ---- int8 wire codec (not in the reference) --------------------------
  * One DL_Q8_SLOT_BYTES slot per chunk of the bucket, in chunk order: fp32 scale at byte 0,
  * int8 values at byte 64 (bytes past the chunk's length stay zero; slots must be zeroed once).

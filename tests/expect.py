@@ -27,3 +27,23 @@ def expected_q8(n, steps=2, cap=MICRO_Q8_CAP):
             oracle.sgd(theta[t], buf[t], g[t], 0.7, 0.9, True, s == 1)
         out[f"theta_s{s}"] = np.concatenate(theta)
     return out
+
+
+def expected_rank_order(n, steps=2, wire="f32"):
+    """The outer step with the replicas' deltas summed in rank order in fp32 (a bf16 wire
+    rounds each delta first and never the sum): oracle.OuterState, micro tree, n replicas --
+    what exchange="a2a" and the direct exchange compute at every n."""
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from oracle import oracle
+
+    spec = get_tree("micro")
+    theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
+    st = oracle.OuterState(theta0)
+    out = {}
+    for s in range(1, steps + 1):
+        inners = [synth.inner_tree(st.theta, s, r) for r in range(n)]
+        st.step(inners, wire)
+        out[f"theta_s{s}"] = np.concatenate(st.theta)
+        out[f"buf_s{s}"] = np.concatenate(st.buf)
+    return out

@@ -127,6 +127,18 @@ class OracleKernels:
         if mom is not None:
             _np(mom)[:] = b
 
+    def shard_reduce_sgd(self, slices, n_slices, theta, mom, lr, momentum, nesterov, first):
+        """Σ over the n slices in rank order, /n (oracle/or_sum_avg), then the shard's SGD."""
+        assert slices.dtype == torch.float32
+        L, s = theta.numel(), _np(slices)
+        g = oracle.sum_avg([np.ascontiguousarray(s[q * L:(q + 1) * L]) for q in range(n_slices)])
+        th = _np(theta).copy()
+        b = _np(mom).copy() if mom is not None else None
+        oracle.sgd(th, b, g, lr, momentum, nesterov, first)
+        _np(theta)[:] = th
+        if mom is not None:
+            _np(mom)[:] = b
+
     def _chunk_range(self, tree, bucket):
         return (0, len(tree.chunks)) if bucket == -1 else tree.bucket_chunks[bucket]
 

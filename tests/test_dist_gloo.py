@@ -19,7 +19,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import PKG, REPO, load_npz, normwise_ok, split
-from expect import MICRO_Q8_CAP, expected_q8
+from expect import MICRO_Q8_CAP, expected_q8, expected_rank_order
 
 MICRO_STEPS = 2
 # stand-in for src/metrics.py Outputs (a pydantic model there); module level so it pickles
@@ -126,14 +126,16 @@ def _worker(rank, world, port, mode, num_stages, out):
             rec[f"inner_s{s}"] = np.concatenate([p.detach().numpy().reshape(-1) for p in inner.parameters()])
         if mode == "dropin_host":
             assert not has_mirror(outer)  # every call took the reference's host semantics
-    elif mode in ("engine", "engine_ar"):
+    elif mode in ("engine", "engine_ar", "engine_a2a"):
         # engine: the default at n > 1, reduce-scatter -> shard SGD -> all-gather;
-        # engine_ar: the replicated variant, all-reduce -> full SGD on every peer
+        # engine_ar: the replicated variant, all-reduce -> full SGD on every peer;
+        # engine_a2a: the sharded step with all_to_all + rank-order reduce (exchange="a2a")
         params = [torch.from_numpy(v.copy()) for v in theta0]
         eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True,
                         group=world_.curr_stage_group, world_size=len(world_.dp_ranks),
-                        bucket_cap_elems=4096, shard=None if mode == "engine" else False)
-        assert eng.sharded == (mode == "engine")
+                        bucket_cap_elems=4096, shard=None if mode != "engine_ar" else False,
+                        exchange="a2a" if mode == "engine_a2a" else "rccl")
+        assert eng.sharded == (mode != "engine_ar") and eng.a2a == (mode == "engine_a2a")
         assert eng.tree.n_buckets > 2
         for s in range(1, MICRO_STEPS + 1):
             th = eng.unpacked(eng.theta)
@@ -257,7 +259,7 @@ def _run(mode, world, num_stages=1):
 
 
 @pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_deferred", "engine",
-                                  "engine_ar", "dropin_host"])
+                                  "engine_ar", "engine_a2a", "dropin_host"])
 def test_two_peers_match_reference_bit_exact(mode):
     g = load_npz("micro_n2.npz")
     recs = _run(mode, 2)
@@ -371,3 +373,25 @@ def test_int8_wire_exchange_matches_oracle(world):
     g = load_npz(f"micro_n{world}.npz")
     err = np.abs(exp["theta_s1"] - g["theta_s1"]).max() / np.abs(g["theta_s1"] - g["theta0"]).max()
     assert err < 2e-2
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_a2a_exchange_is_bit_exact_against_rank_order_oracle(world):
+    """exchange="a2a" over a real process group: the all_to_all hands every peer the n copies
+    of its shard and the reduce sums them in rank order, so every replica ends bit-identical
+    to the oracle's rank-order restatement at any n (the reduce-scatter's sum order is the
+    transport's, normwise only) -- and still within 1e-6 normwise of the reference's gloo run."""
+    from diloco_amd.trees import get_tree
+
+    exp = expected_rank_order(world)
+    recs = _run("engine_a2a", world)
+    for rec in recs:
+        for s in (1, 2):
+            for k in ("theta", "buf"):
+                assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (k, s)
+            assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), s
+    numels = get_tree("micro").numels()
+    g = load_npz(f"micro_n{world}.npz")
+    for s in (1, 2):
+        for a, b in zip(split(exp[f"theta_s{s}"], numels), split(g[f"theta_s{s}"], numels)):
+            assert normwise_ok(a, b, 1e-6), s

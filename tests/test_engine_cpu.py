@@ -31,12 +31,13 @@ def _flat(ts):
     return np.concatenate([t.reshape(-1).numpy() for t in ts])
 
 
-@pytest.mark.parametrize("shard", [False, True])
-def test_single_replica_engine_matches_reference(shard):
+@pytest.mark.parametrize("shard,exchange", [(False, "rccl"), (True, "rccl"), (None, "a2a")])
+def test_single_replica_engine_matches_reference(shard, exchange):
     spec, params = _micro_params()
     g = load_npz("micro_n1.npz")
-    e = OuterSync(params, world_size=1, bucket_cap_elems=4096, shard=shard, fuse_single=False)
-    assert e.sharded == shard and e.tree.n_buckets > 2
+    e = OuterSync(params, world_size=1, bucket_cap_elems=4096, shard=shard, fuse_single=False,
+                  exchange=exchange)
+    assert e.sharded == (shard is not False) and e.tree.n_buckets > 2
     for s in (1, 2):
         vals = synth.inner_tree([t.numpy().reshape(-1) for t in e.unpacked(e.theta)], s, 0)
         for p, v in zip(params, vals):
@@ -55,6 +56,11 @@ def test_engine_argument_errors():
         OuterSync(params, world_size=1, wire_dtype=torch.float16)
     with pytest.raises(ValueError, match="Nesterov momentum requires a momentum"):
         OuterSync(params, world_size=1, momentum=0.0, nesterov=True)
+    with pytest.raises(ValueError, match="exchanges the f32 or bf16 wire"):
+        OuterSync(params, world_size=2, wire_dtype=torch.int8, exchange="a2a")
+    with pytest.raises(ValueError, match="shard=False contradicts"):
+        OuterSync(params, world_size=2, shard=False, exchange="a2a")
+    assert OuterSync(params, world_size=4, wire_dtype=torch.bfloat16, exchange="a2a").sharded
     with pytest.raises(ValueError, match="at least one parameter"):
         OuterSync([], world_size=1)
     e = OuterSync(params, world_size=1, shard=True)

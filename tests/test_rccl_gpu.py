@@ -120,6 +120,21 @@ def _worker(rank, port, out):
         rec[f"sh_theta_s{s}"] = _flat(es.unpacked(es.theta))
         rec[f"sh_buf_s{s}"] = _flat(es.unpacked(es.momentum_full()))
         rec[f"sh_inner_s{s}"] = _flat(sp)
+    # 6. the ordered sharded variant (all_to_all -> dl_shard_reduce_sgd -> all_gather), fp32
+    #    on the micro tree vs the reference, bf16 vs the oracle's rank-order restatement
+    for wire, tag in ((torch.float32, "a2a"), (torch.bfloat16, "a2a_bf16")):
+        ap = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"), shapes)]
+        ea = OuterSync(ap, world_size=1, bucket_cap_elems=4096, exchange="a2a", wire_dtype=wire)
+        assert ea.sharded and ea.a2a and not ea._local() and ea.tree.n_buckets > 2
+        for s in (1, 2):
+            th = [t.reshape(-1) for t in ea.unpacked(ea.theta)]
+            synth.inner_tree_device(th, s, 0, out=[p.view(-1) for p in ap])
+            ea.step()
+            torch.cuda.synchronize()
+            rec[f"{tag}_theta_s{s}"] = _flat(ea.unpacked(ea.theta))
+            rec[f"{tag}_buf_s{s}"] = _flat(ea.unpacked(ea.momentum_full()))
+            rec[f"{tag}_inner_s{s}"] = _flat(ap)
+        ea.close()
     np.savez(os.path.join(out, "rccl.npz"), **rec)
     dist.destroy_process_group()
 
@@ -141,6 +156,15 @@ def test_rccl_single_rank_transport_bit_exact():
         assert rec[f"sh_theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
         assert rec[f"sh_buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes()
         assert rec[f"sh_inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+    from expect import expected_rank_order
+
+    exp = expected_rank_order(1, wire="bf16")
+    for s in (1, 2):
+        for k in ("theta", "buf"):
+            assert rec[f"a2a_{k}_s{s}"].tobytes() == g[f"{k}_s{s}"].tobytes(), (k, s)
+            assert rec[f"a2a_bf16_{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (k, s)
+        assert rec[f"a2a_inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+        assert rec[f"a2a_bf16_inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes()
 
 
 def _worker_q8(rank, port, out):
