@@ -279,6 +279,8 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
                              + (f", tiles of {eng.tile_chunks} chunks" if eng.tile_chunks
                                 else ", whole-range launches")) if single
                        else "direct peer-access exchange (IPC, dl_xgmi_reduce_sgd)" if eng.xgmi
+                       else "all_to_all -> rank-order reduce + shard SGD (dl_shard_reduce_sgd) "
+                            "-> all_gather" if eng.a2a
                        else "reduce_scatter -> shard SGD -> all_gather" if eng.sharded
                        else "all_reduce -> replicated SGD")}
     fused_name = "delta_pack_sgd" if keep_wire else "delta_sgd"
@@ -390,7 +392,8 @@ def run_tree(spec, dev, ws, rank, steps, warmup, wire, cap, fuse=False, b2b_loop
         # all-reduce: 2(n-1)/n · wire bytes; sharded: (n-1)/n · wire (RS) + (n-1)/n · 4 B (AG of θ)
         frac = (ws - 1) / ws * eng.tree.total
         bus = frac * (wb + 4) if eng.sharded else 2.0 * frac * wb
-        name = ("rccl reduce_scatter + all_gather (all buckets, back to back)" if eng.sharded
+        name = ("rccl all_to_all + all_gather (all buckets, back to back)" if eng.a2a
+                else "rccl reduce_scatter + all_gather (all buckets, back to back)" if eng.sharded
                 else "rccl all_reduce (all buckets, back to back)")
         res["roofline"] = dict(kernel_entry(bus, ar_ms, bound="xgmi",
                                             peak=(ws - 1) * XGMI_LINK_GBS),
@@ -588,13 +591,15 @@ def parity_xgmi(dev, ws, rank, exchange="xgmi"):
             "ok": bool(worst <= 1e-6 and identical and inner_ok)}
 
 
-def parity_sharded(dev, ws, rank):
-    """The sharded step (reduce-scatter -> dl_shard_sgd -> all-gather -> dl_scatter) against
-    the replicated one (all-reduce -> dl_unpack_sgd) on the tiny tree, 2 outer steps: θ,
-    momentum and inner normwise <= 1e-6 per tensor (bit-exact where the two collectives sum in
-    the same order), every replica bit-identical."""
+def parity_sharded(dev, ws, rank, exchange="rccl", wire=torch.float32):
+    """The sharded step (reduce-scatter -> dl_shard_sgd -> all-gather -> dl_scatter; with
+    exchange="a2a" all_to_all -> dl_shard_reduce_sgd -> all-gather) against the replicated one
+    (all-reduce -> dl_unpack_sgd, fp32 wire) on the tiny tree, 2 outer steps: θ, momentum and
+    inner normwise <= 1e-6 per tensor (bit-exact where the two sum in the same order; a bf16
+    wire within 2^-8 of the fp32 step, the codec's one rounding -- the a2a reduce never
+    re-rounds the sum), every replica bit-identical."""
     spec = get_tree("tiny")
-    ea = build(spec, dev, rank, torch.float32, 1 << 20, shard=True)
+    ea = build(spec, dev, rank, wire, 1 << 20, shard=True, exchange=exchange)
     eb = build(spec, dev, rank, torch.float32, 1 << 20, shard=False)
     for s in (1, 2):
         for e in (ea, eb):
@@ -619,10 +624,12 @@ def parity_sharded(dev, ws, rank):
     buckets = ea.tree.n_buckets
     ea.close()
     eb.close()
-    return {"tree": "tiny", "buckets": buckets, "steps": 2,
+    tol = 1e-6 if wire == torch.float32 else 2.0 ** -8
+    return {"tree": "tiny", "buckets": buckets, "steps": 2, "exchange": exchange,
+            "wire": "bf16" if wire == torch.bfloat16 else "f32",
             "sharded_vs_replicated_normwise_err": worst, "bit_exact": exact,
-            "tolerance": 1e-6, "inner_is_theta": inner_ok, "replicas_identical": identical,
-            "ok": bool(worst <= 1e-6 and identical and inner_ok)}
+            "tolerance": tol, "inner_is_theta": inner_ok, "replicas_identical": identical,
+            "ok": bool(worst <= tol and identical and inner_ok)}
 
 
 def run_q8(spec, dev, ws, rank, steps, warmup, cap):
@@ -1396,6 +1403,9 @@ def main():
                 leg(f"{es.name}_bf16_wire", run_tree, es, dev, ws, rank, ks, 1, torch.bfloat16,
                     cap)
                 leg(f"{es.name}_int8_wire", run_q8, es, dev, ws, rank, ks, 1, cap)  # §8f row 4
+                if ws > 1:  # config #5 with the ordered exchange: bf16 slices summed in fp32
+                    leg(f"{es.name}_bf16_a2a", run_tree, es, dev, ws, rank, ks, 1,
+                        torch.bfloat16, cap, False, False, True, "a2a")
         if ws > 1:
             # RCCL's own all-reduce rate on the headline's bytes (the exchange's yardstick)
             ref = leg("rccl_allreduce_ref", rccl_reference, dev, ws, rank,
@@ -1415,6 +1425,9 @@ def main():
             # bucket size for the xGMI pipeline: 64 MiB buckets (more overlap, more calls)
             leg(f"{spec.name}_bucket64MiB", run_tree, spec, dev, ws, rank, a.steps, a.warmup,
                 wire, 16 << 20, False, False)
+            # the ordered sharded step: all_to_all + rank-order reduce (deterministic, same bus)
+            leg(f"{spec.name}_a2a", run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, cap,
+                False, False, True, "a2a")
             leg(f"{spec.name}_dp_grad_sync", gradsync_rate, spec, dev, ws, rank,
                 max(3, a.steps // 2), brief=False)
             if ws >= 4 and ws % 2 == 0:  # two concurrent disjoint DP groups (S = 2)
@@ -1425,6 +1438,9 @@ def main():
             leg("bf16", parity_check, dev, ws, rank, torch.bfloat16, into=parity, brief=False)
             leg("int8", parity_q8, dev, ws, rank, into=parity, brief=False)
             leg("sharded", parity_sharded, dev, ws, rank, into=parity, brief=False)
+            leg("a2a", parity_sharded, dev, ws, rank, "a2a", into=parity, brief=False)
+            leg("a2a_bf16", parity_sharded, dev, ws, rank, "a2a", torch.bfloat16, into=parity,
+                brief=False)
         if not a.no_dropin:
             em.line["dropin_pcie"] = leg("dropin_pcie", dropin_rate, spec, dev, ws, rank, 5,
                                          into={}, brief=False)

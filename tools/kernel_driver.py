@@ -40,9 +40,17 @@ def main():
     q8 = OuterSync(params, world_size=1, wire_dtype=torch.int8, bucket_cap_elems=0)
     sh = OuterSync(params, world_size=1, shard=True, bucket_cap_elems=0)
     xg = OuterSync(params, world_size=1, exchange="xgmi")  # n = 1: the fused kernel, local
-    for e in (q8, sh, xg):
+    a2 = OuterSync(params, world_size=1, exchange="a2a", bucket_cap_elems=0)
+    for e in (q8, sh, xg, a2):
         for _ in range(reps + 1):
             e.step()
+    # dl_shard_reduce_sgd as an 8-peer rank would run it: 8 slices of an eighth of the tree
+    L = (sum(p.numel() for p in params) // 8) // 64 * 64
+    slices = torch.randn(8 * L, device=dev) * 1e-3
+    th8, m8 = torch.randn(L, device=dev), torch.zeros(L, device=dev)
+    for i in range(reps + 1):
+        eng.k.shard_reduce_sgd(slices, 8, th8, m8, 0.7, 0.9, True, i == 0)
+    del slices, th8, m8
     # the per-step DP gradient sync at one replica (dl_gather -> identity -> dl_unpack_avg),
     # one bucket so each launch covers the tree
     from diloco_amd.gradsync import GradSync

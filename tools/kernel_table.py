@@ -30,7 +30,11 @@ def algorithmic(kernel, P, n_chunks):
              "delta_q8": 8 * P + slot, "q8_reduce": 2 * slot,
              "unpack_sgd_q8": slot + 20 * P, "unpack_sgd_q8_first": slot + 16 * P,
              "xgmi_reduce_sgd": 20 * P, "xgmi_delta_sgd": 20 * P,
-             "serialize_f32": 8 * ACT, "serialize_bf16": 6 * ACT}
+             "serialize_f32": 8 * ACT, "serialize_bf16": 6 * ACT,
+             # n = 1 (the whole tree, 20 B); n = 8: 8 fp32 slices of an eighth + θ, buf
+             "shard_reduce_sgd": 20 * P, "shard_reduce_sgd_first": 16 * P,
+             "shard_reduce_sgd_n8": (P // 8 // 64 * 64) * (8 * 4 + 16),
+             "shard_reduce_sgd_n8_first": (P // 8 // 64 * 64) * (8 * 4 + 12)}
     return table.get(kernel)
 
 

@@ -23,7 +23,8 @@ def short(name):
              "DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd",
              "UnpackAvg": "unpack_avg", "DeltaSgd": "delta_sgd", "Gather": "gather",
              "Scatter": "scatter", "k_fill_synth": "fill_synth",
-             "k_serialize_f32x4": "serialize_f32", "k_serialize<unsigned short>": "serialize_bf16"}
+             "k_serialize_f32x4": "serialize_f32", "k_serialize<unsigned short>": "serialize_bf16",
+             "k_slices_sgd": "shard_reduce_sgd"}
     if "k_xgmi_reduce_sgd" in name and ", true>" in name:
         return "xgmi_delta_sgd"  # the pack-free variant (exchange="xgmi_inner")
     for k, v in names.items():
@@ -32,8 +33,12 @@ def short(name):
             # template list (k_walk's trailing arguments are the load / store policy)
             body = "UnpackSgd" if k == "k_flat" else k
             m = re.search(re.escape(body) + r"<([^<>]*)>", name)
-            first = (k in ("UnpackSgd", "k_flat", "DeltaSgd", "DeltaPackSgd", "UnpackSgdQ8")
+            first = (k in ("UnpackSgd", "k_flat", "DeltaSgd", "DeltaPackSgd", "UnpackSgdQ8",
+                           "k_slices_sgd")
                      and m is not None and m.group(1).split(",")[-1].strip() == "1")
+            if k == "k_slices_sgd" and m is not None:  # the slice count is its first argument
+                nsl = m.group(1).split(",")[0].strip()
+                v += "" if nsl == "1" else f"_n{nsl}"
             return v + ("_first" if first else "")
     return None
 
