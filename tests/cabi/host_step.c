@@ -8,6 +8,9 @@
  *           communicator the library creates (dl_rccl_load, dl_comm_unique_id, dl_comm_init)
  *   step 4: the sharded step per bucket: dl_delta_pack -> dl_reduce_scatter -> dl_shard_sgd
  *           -> dl_all_gather -> dl_scatter on the same communicator
+ *   step 5: the ordered sharded step (OuterSync(exchange="a2a")) per bucket: dl_delta_pack ->
+ *           the all_to_all as grouped dl_send / dl_recv (one rank: its own slice) ->
+ *           dl_shard_reduce_sgd -> dl_all_gather -> dl_scatter
  * plus an argument error (unbound slot) reported through the return code and dl_last_error.
  * Built by __graft_entry__.build() (gcc, no GPU needed); run by tests/test_cabi_host.py.
  * Exit status 0 = every byte equal. */
@@ -110,7 +113,7 @@ int main(void) {
   HIP(hipMalloc((void**)&d_thshard, total * 4));
   HIP(hipMalloc((void**)&d_momshard, total * 4));
   int ok = 1;
-  for (int step = 1; step <= 4; ++step) {
+  for (int step = 1; step <= 5; ++step) {
     /* inner = θ + noise (the synthetic stand-in for H inner steps) */
     for (int t = 0; t < NT; ++t) {
       or_fill_synth(h_in[t], NUMEL[t], (uint64_t)(1000 * step), (uint64_t)t, 0.0f, 1e-3f,
@@ -133,6 +136,23 @@ int main(void) {
         DL(dl_allreduce(d_wire + lo, hi - lo, DL_F32, comm, NULL));
         DL(dl_unpack_sgd(tree, b, d_wire, DL_F32, 1, d_theta, d_mom, lr, mom, 1, 0, 0, NULL));
       }
+    } else if (step == 5) {
+      HIP(hipMemcpy(d_thshard, d_theta, total * 4, hipMemcpyDeviceToDevice));
+      HIP(hipMemcpy(d_momshard, d_mom, total * 4, hipMemcpyDeviceToDevice));
+      for (int32_t b = 0; b < nbkt; ++b) {
+        int64_t lo = 0, hi = 0;
+        DL(dl_tree_bucket_range(tree, b, &lo, &hi));
+        DL(dl_delta_pack(tree, b, 0, d_theta, d_wire, DL_F32, NULL));
+        DL(dl_group_start());
+        DL(dl_send(d_wire + lo, hi - lo, DL_F32, 0, comm, NULL));
+        DL(dl_recv(d_gshard + lo, hi - lo, DL_F32, 0, comm, NULL));
+        DL(dl_group_end());
+        DL(dl_shard_reduce_sgd(d_gshard + lo, DL_F32, 1, hi - lo, d_thshard + lo, d_momshard + lo,
+                               lr, mom, 1, 0, NULL));
+        DL(dl_all_gather(d_thshard + lo, d_theta + lo, hi - lo, DL_F32, comm, NULL));
+        DL(dl_scatter(tree, b, d_theta, 0, NULL));
+      }
+      HIP(hipMemcpy(d_mom, d_momshard, total * 4, hipMemcpyDeviceToDevice));
     } else {
       HIP(hipMemcpy(d_thshard, d_theta, total * 4, hipMemcpyDeviceToDevice));
       HIP(hipMemcpy(d_momshard, d_mom, total * 4, hipMemcpyDeviceToDevice));
