@@ -81,14 +81,17 @@ def test_automatic_variant_choice():
         assert lo % 256 == 0 and (hi - lo) % 256 == 0
 
 
-@pytest.mark.parametrize("src_shard,dst_shard", [(False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("src_shard,dst_shard", [(False, True), (True, False), (True, True),
+                                               (False, "a2a"), ("a2a", False)])
 def test_checkpoint_resume_across_variants(src_shard, dst_shard):
     """state_dict after step 1 of one engine, loaded into a fresh engine of another variant /
     bucket layout: step 2 from the restored state equals the reference's step 2."""
+    def kw(v):
+        return {"shard": None, "exchange": "a2a"} if v == "a2a" else {"shard": v}
+
     spec, params = _micro_params()
     g = load_npz("micro_n1.npz")
-    a = OuterSync(params, world_size=1, bucket_cap_elems=4096, shard=src_shard,
-                  fuse_single=False)
+    a = OuterSync(params, world_size=1, bucket_cap_elems=4096, fuse_single=False, **kw(src_shard))
     vals = synth.inner_tree([t.numpy().reshape(-1) for t in a.unpacked(a.theta)], 1, 0)
     for p, v in zip(params, vals):
         p.copy_(torch.from_numpy(v).view(p.shape))
@@ -96,8 +99,8 @@ def test_checkpoint_resume_across_variants(src_shard, dst_shard):
     st = a.state_dict()
     assert st["steps"] == 1 and len(st["momentum"]) == len(params)
     _, params2 = _micro_params()
-    b = OuterSync(params2, world_size=1, bucket_cap_elems=8192, shard=dst_shard,
-                  fuse_single=False)
+    b = OuterSync(params2, world_size=1, bucket_cap_elems=8192, fuse_single=False,
+                  **kw(dst_shard))
     b.load_state_dict(st)
     assert _flat(params2).tobytes() == g["theta_s1"].tobytes()  # inner = θ_1
     vals = synth.inner_tree([t.numpy().reshape(-1) for t in b.unpacked(b.theta)], 2, 0)
