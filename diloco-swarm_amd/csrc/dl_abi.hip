@@ -557,6 +557,21 @@ DL_API int dl_shard_reduce_sgd(const void* slices, int32_t wire_dtype, int32_t n
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_shard_reduce_sgd");
 }
 
+DL_API int dl_shard_reduce_avg(const void* slices, int32_t wire_dtype, int32_t n_slices,
+                               int64_t len, float* out, dl_stream_t s) {
+  if (len < 0 || len % 4 != 0)
+    return fail(DL_E_ARG, "dl_shard_reduce_avg: len %lld (a multiple of 4)", (long long)len);
+  if (n_slices < 1) return fail(DL_E_ARG, "dl_shard_reduce_avg: n_slices %d", n_slices);
+  if (len == 0) return DL_OK;
+  DL_TRY(check_packed(slices, "dl_shard_reduce_avg", "slices"));
+  DL_TRY(check_dtype(wire_dtype, "dl_shard_reduce_avg"));
+  DL_TRY(check_packed(out, "dl_shard_reduce_avg", "out"));
+  dl::SgdArgs a{0.f, 0.f, 0, 0};
+  hipError_t e = dl::launch_slices_sgd(slices, wire_dtype, n_slices, len, out, nullptr, a,
+                                       static_cast<hipStream_t>(s), true);
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_shard_reduce_avg");
+}
+
 DL_API int dl_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
   if (!ptr || !handle || !offset) return fail(DL_E_ARG, "dl_ipc_handle: null argument");
   void* base = nullptr;

@@ -75,7 +75,8 @@ hipError_t launch_delta_pack_sgd(const Launch& L, int inner_slot, float* outer, 
 hipError_t launch_shard_sgd(const void* wire, int wire_dtype, int divisor, float* outer, float* mom,
                             int64_t n, SgdArgs a, hipStream_t s);
 hipError_t launch_slices_sgd(const void* slices, int wire_dtype, int32_t n, int64_t len,
-                             float* outer, float* mom, SgdArgs a, hipStream_t s);
+                             float* outer, float* mom, SgdArgs a, hipStream_t s,
+                             bool avg_only = false);
 hipError_t launch_delta_q8(const Launch& L, int inner_slot, const float* outer, uint8_t* slots);
 hipError_t launch_unpack_sgd_q8(const Launch& L, const uint8_t* slots, float* outer, float* mom,
                                 SgdArgs a, int inner_slot);

@@ -671,6 +671,7 @@ hipError_t launch_shard_sgd(const void* wire, int wire_dtype, int divisor, float
 // rank order -- the order of oracle/or_sum_avg and dl_xgmi_reduce_sgd, identical on every
 // rank whatever the transport -- then dl_shard_sgd's SGD on this peer's θ and momentum shards.
 // Reads n·sizeof(W) + 8 B, writes 8 B per shard element. N = 0: n read at run time (n > 8).
+// MODE 3 (dl_shard_reduce_avg, the ordered DP gradient sync): no SGD -- `th` receives g.
 constexpr int kSU = 2;                          // float4 rows per lane
 constexpr int64_t kSliceStep = kThreads * kSU * 4;  // 2048 elements per workgroup and round
 template <int N, typename W, int MODE>
@@ -692,7 +693,7 @@ __global__ void __launch_bounds__(kThreads)
         if (v < nv) {
 #pragma unroll
           for (int q = 0; q < N; ++q) w[q][u] = WireIO<W>::template ld4<true>(slices + q * len + base, v);
-          t[u] = ldf4<true>(t0, v);
+          if (MODE != 3) t[u] = ldf4<true>(t0, v);
           if (MODE == 2) m[u] = ldf4<true>(m0, v);
         }
       }
@@ -709,7 +710,7 @@ __global__ void __launch_bounds__(kThreads)
       for (int u = 0; u < kSU; ++u) {
         const int v = u * kThreads + int(threadIdx.x);
         if (v < nv) {
-          t[u] = ldf4<true>(t0, v);
+          if (MODE != 3) t[u] = ldf4<true>(t0, v);
           if (MODE == 2) m[u] = ldf4<true>(m0, v);
           g[u] = WireIO<W>::template ld4<true>(slices + base, v);
           for (int q = 1; q < nn; ++q) {
@@ -724,12 +725,16 @@ __global__ void __launch_bounds__(kThreads)
       const int v = u * kThreads + int(threadIdx.x);
       if (v < nv) {
         const float4 gg = nn > 1 ? div4(g[u], float(nn)) : g[u];
-        sgd1<MODE>(gg.x, m[u].x, t[u].x, a);
-        sgd1<MODE>(gg.y, m[u].y, t[u].y, a);
-        sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
-        sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
-        stf4<kStNT>(t0, v, t[u]);
-        if (MODE != 0) stf4<kStNT>(m0, v, m[u]);
+        if constexpr (MODE == 3) {
+          stf4<kStNT>(t0, v, gg);
+        } else {
+          sgd1<MODE>(gg.x, m[u].x, t[u].x, a);
+          sgd1<MODE>(gg.y, m[u].y, t[u].y, a);
+          sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
+          sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
+          stf4<kStNT>(t0, v, t[u]);
+          if (MODE != 0) stf4<kStNT>(m0, v, m[u]);
+        }
       }
     }
   }
@@ -737,10 +742,12 @@ __global__ void __launch_bounds__(kThreads)
 
 template <int N, typename W>
 static hipError_t slices_sgd_n(const W* w, int32_t n, int64_t len, float* th, float* mom,
-                               SgdArgs a, hipStream_t s) {
+                               SgdArgs a, hipStream_t s, bool avg_only) {
   const int64_t blocks = (len + kSliceStep - 1) / kSliceStep;
   const int32_t grid = int32_t(blocks < (1 << 20) ? blocks : (1 << 20));
-  if (a.momentum == 0.f)
+  if (avg_only)
+    hipLaunchKernelGGL((k_slices_sgd<N, W, 3>), dim3(grid), dim3(kThreads), 0, s, w, n, len, th, mom, a);
+  else if (a.momentum == 0.f)
     hipLaunchKernelGGL((k_slices_sgd<N, W, 0>), dim3(grid), dim3(kThreads), 0, s, w, n, len, th, mom, a);
   else if (a.first)
     hipLaunchKernelGGL((k_slices_sgd<N, W, 1>), dim3(grid), dim3(kThreads), 0, s, w, n, len, th, mom, a);
@@ -751,26 +758,27 @@ static hipError_t slices_sgd_n(const W* w, int32_t n, int64_t len, float* th, fl
 
 template <typename W>
 static hipError_t slices_sgd_t(const W* w, int32_t n, int64_t len, float* th, float* mom,
-                               SgdArgs a, hipStream_t s) {
+                               SgdArgs a, hipStream_t s, bool avg) {
   switch (n) {
-    case 1: return slices_sgd_n<1>(w, n, len, th, mom, a, s);
-    case 2: return slices_sgd_n<2>(w, n, len, th, mom, a, s);
-    case 3: return slices_sgd_n<3>(w, n, len, th, mom, a, s);
-    case 4: return slices_sgd_n<4>(w, n, len, th, mom, a, s);
-    case 5: return slices_sgd_n<5>(w, n, len, th, mom, a, s);
-    case 6: return slices_sgd_n<6>(w, n, len, th, mom, a, s);
-    case 7: return slices_sgd_n<7>(w, n, len, th, mom, a, s);
-    case 8: return slices_sgd_n<8>(w, n, len, th, mom, a, s);
-    default: return slices_sgd_n<0>(w, n, len, th, mom, a, s);
+    case 1: return slices_sgd_n<1>(w, n, len, th, mom, a, s, avg);
+    case 2: return slices_sgd_n<2>(w, n, len, th, mom, a, s, avg);
+    case 3: return slices_sgd_n<3>(w, n, len, th, mom, a, s, avg);
+    case 4: return slices_sgd_n<4>(w, n, len, th, mom, a, s, avg);
+    case 5: return slices_sgd_n<5>(w, n, len, th, mom, a, s, avg);
+    case 6: return slices_sgd_n<6>(w, n, len, th, mom, a, s, avg);
+    case 7: return slices_sgd_n<7>(w, n, len, th, mom, a, s, avg);
+    case 8: return slices_sgd_n<8>(w, n, len, th, mom, a, s, avg);
+    default: return slices_sgd_n<0>(w, n, len, th, mom, a, s, avg);
   }
 }
 
+// avg_only: out (`outer`) = Σ/n, no SGD, `mom` unused (dl_shard_reduce_avg)
 hipError_t launch_slices_sgd(const void* slices, int wire_dtype, int32_t n, int64_t len,
-                             float* outer, float* mom, SgdArgs a, hipStream_t s) {
+                             float* outer, float* mom, SgdArgs a, hipStream_t s, bool avg_only) {
   if (len <= 0) return hipSuccess;
   if (wire_dtype == DL_BF16)
-    return slices_sgd_t(static_cast<const bf16_t*>(slices), n, len, outer, mom, a, s);
-  return slices_sgd_t(static_cast<const float*>(slices), n, len, outer, mom, a, s);
+    return slices_sgd_t(static_cast<const bf16_t*>(slices), n, len, outer, mom, a, s, avg_only);
+  return slices_sgd_t(static_cast<const float*>(slices), n, len, outer, mom, a, s, avg_only);
 }
 
 hipError_t launch_delta_sgd(const Launch& L, int inner_slot, float* outer, float* mom, SgdArgs a) {

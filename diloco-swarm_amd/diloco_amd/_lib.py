@@ -73,6 +73,7 @@ SIGNATURES = {
     "dl_shard_reduce_sgd": (
         ctypes.c_int, [_vp, _i32, _i32, _i64, _vp, _vp, _f32, _f32, _i32, _i32, _vp],
     ),
+    "dl_shard_reduce_avg": (ctypes.c_int, [_vp, _i32, _i32, _i64, _vp, _vp]),
     "dl_delta_q8": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
     "dl_q8_reduce": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _vp]),
     "dl_unpack_sgd_q8": (

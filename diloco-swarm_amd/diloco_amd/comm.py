@@ -142,6 +142,9 @@ class RecvThread:
 # product). "gloo" exists for multi-process tests that share one GPU (RCCL refuses two ranks
 # on one device); the kernels are the same HIP kernels either way.
 DP_BACKEND = os.environ.get("DILOCO_DP_BACKEND", "nccl")
+# The device-gradient average's exchange (gradsync.GradSync): "rccl" = all_reduce; "a2a" =
+# all_to_all + rank-order average + all_gather (deterministic, bit-exact vs the oracle at any n)
+DP_EXCHANGE = os.environ.get("DILOCO_DP_EXCHANGE", "rccl")
 
 
 class DPSync:
@@ -200,7 +203,8 @@ class DPSync:
                 p.grad = torch.zeros_like(p)
         gs = self._grad_syncs.get(id(model))
         if gs is None or not gs.matches(params):
-            gs = GradSync(params, self.dp_group(params[0].device), num_peers)
+            gs = GradSync(params, self.dp_group(params[0].device), num_peers,
+                          exchange=DP_EXCHANGE)
             self._grad_syncs[id(model)] = gs
         gs.sync()
 

@@ -101,6 +101,11 @@ class HipKernels:
                   int(n_slices), theta.numel(), theta.data_ptr(), _ptr(mom), float(lr),
                   float(momentum), int(nesterov), int(first), _s(theta))
 
+    def shard_reduce_avg(self, slices, n_slices, out) -> None:
+        """out = Σ of the n_slices equal slices in rank order / n (fp32 out, out's length)."""
+        _lib.call("dl_shard_reduce_avg", slices.data_ptr(), wire_code(slices.dtype),
+                  int(n_slices), out.numel(), out.data_ptr(), _s(out))
+
     def xgmi_reduce_sgd(self, wires, thetas, n, rank, lo, length, mom, lr, momentum, nesterov,
                         first, device=None) -> None:
         """Direct exchange on this rank's shard (wires / thetas: uint64 arrays of the n peers'

@@ -210,6 +210,12 @@ DL_API int dl_shard_reduce_sgd(const void* slices, int32_t wire_dtype, int32_t n
                                int64_t len, float* outer, float* mom, float lr, float momentum,
                                int32_t nesterov, int32_t first_step, dl_stream_t stream);
 
+/* The same rank-order average without the SGD, for the ordered per-step DP gradient sync
+ * (GradSync(exchange="a2a"), src/comm.py:120-123 on device grads): out[k] =
+ * ((s_0[k] + s_1[k]) + ... + s_{n-1}[k]) / n in fp32. len a multiple of 4; 16-B aligned. */
+DL_API int dl_shard_reduce_avg(const void* slices, int32_t wire_dtype, int32_t n_slices,
+                               int64_t len, float* out, dl_stream_t stream);
+
 /* ---- int8 wire codec (not in the reference) --------------------------
  * One DL_Q8_SLOT_BYTES slot per chunk of the bucket, in chunk order: fp32 scale at byte 0,
  * int8 values at byte 64 (bytes past the chunk's length stay zero; slots must be zeroed once).

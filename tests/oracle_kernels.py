@@ -139,6 +139,12 @@ class OracleKernels:
         if mom is not None:
             _np(mom)[:] = b
 
+    def shard_reduce_avg(self, slices, n_slices, out):
+        assert slices.dtype == torch.float32
+        L, s = out.numel(), _np(slices)
+        _np(out)[:] = oracle.sum_avg([np.ascontiguousarray(s[q * L:(q + 1) * L])
+                                      for q in range(n_slices)])
+
     def _chunk_range(self, tree, bucket):
         return (0, len(tree.chunks)) if bucket == -1 else tree.bucket_chunks[bucket]
 

@@ -58,6 +58,25 @@ def test_shard_reduce_sgd_matches_oracle(wire, n, momentum, nesterov):
             assert dm.cpu().numpy().tobytes() == rbuf.tobytes(), length
 
 
+@pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 11])
+def test_shard_reduce_avg_matches_oracle(wire, n):
+    """dl_shard_reduce_avg (GradSync(exchange="a2a")'s reduce) == oracle.sum_avg, bit-exact,
+    IEEE specials included (signed zeros survive: no SGD arithmetic touches the average)."""
+    from diloco_amd.kernels import default_kernels
+
+    k = default_kernels()
+    for length in (4, 2048 + 4, 3 * 2048 * 256 + 64 * 7 + 12):
+        sl = [synth.values(70 + q, length, length, 0.0, 1.0) for q in range(n)]
+        sl[0][:4] = [-0.0, 0.0, np.inf, -1e-40]
+        if wire == torch.bfloat16:
+            sl = [oracle.bf16_round(x) for x in sl]
+        out = torch.full((length,), 7.0, device=DEV)
+        k.shard_reduce_avg(torch.from_numpy(np.concatenate(sl)).to(DEV).to(wire), n, out)
+        torch.cuda.synchronize()
+        assert out.cpu().numpy().tobytes() == oracle.sum_avg(sl).tobytes(), length
+
+
 def _emulated_a2a_steps(n, wire, steps=2):
     """n replicas of the micro tree on this GPU, exchange="a2a", collectives emulated:
     all_to_all = peer r receives slice r of every rank's wire bucket, in rank order;

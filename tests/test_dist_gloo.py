@@ -183,7 +183,7 @@ def _worker(rank, world, port, mode, num_stages, out):
             eng.step()
             rec[f"theta_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(eng.theta)])
             rec[f"inner_s{s}"] = np.concatenate([p.numpy().reshape(-1) for p in params])
-    elif mode == "gradsync":
+    elif mode in ("gradsync", "gradsync_a2a"):
         from diloco_amd.gradsync import GradSync
 
         g = torch.Generator().manual_seed(100 + rank)
@@ -194,7 +194,8 @@ def _worker(rank, world, port, mode, num_stages, out):
         for r in ref:  # the reference's loop, src/comm.py:120-123
             dist.all_reduce(r, op=dist.ReduceOp.SUM, group=world_.curr_stage_group)
             r /= len(world_.dp_ranks)
-        gs = GradSync(params, world_.curr_stage_group, len(world_.dp_ranks), bucket_cap_elems=4096)
+        gs = GradSync(params, world_.curr_stage_group, len(world_.dp_ranks), bucket_cap_elems=4096,
+                      exchange="a2a" if mode == "gradsync_a2a" else "rccl")
         gs.sync()
         rec["got"] = np.concatenate([p.grad.numpy() for p in params])
         rec["ref"] = np.concatenate([r.numpy() for r in ref])
@@ -395,3 +396,19 @@ def test_a2a_exchange_is_bit_exact_against_rank_order_oracle(world):
     for s in (1, 2):
         for a, b in zip(split(exp[f"theta_s{s}"], numels), split(g[f"theta_s{s}"], numels)):
             assert normwise_ok(a, b, 1e-6), s
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gradsync_a2a_is_bit_exact_against_rank_order_oracle(world):
+    """GradSync(exchange="a2a"): all_to_all -> rank-order average -> all_gather; every rank's
+    grads end equal to oracle.sum_avg of all ranks' grads, bit for bit, at any n."""
+    from oracle import oracle
+
+    sizes = (1, 3, 5000, 64, 4097)
+    grads = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(100 + r)
+        grads.append(np.concatenate([torch.randn(n, generator=g).numpy() for n in sizes]))
+    want = oracle.sum_avg(grads)
+    for rec in _run("gradsync_a2a", world):
+        assert rec["got"].tobytes() == want.tobytes()

@@ -135,6 +135,13 @@ def _worker(rank, port, out):
             rec[f"{tag}_buf_s{s}"] = _flat(ea.unpacked(ea.momentum_full()))
             rec[f"{tag}_inner_s{s}"] = _flat(ap)
         ea.close()
+    # 7. the ordered DP grad sync (GradSync(exchange="a2a")): identity average through RCCL
+    for p in gp:
+        p.grad = torch.randn(p.numel(), generator=g).cuda()
+    before = [p.grad.clone() for p in gp]
+    GradSync(gp, None, 1, bucket_cap_elems=4096, exchange="a2a").sync()
+    torch.cuda.synchronize()
+    rec["gradsync_a2a_equal"] = np.array([all(torch.equal(a, p.grad) for a, p in zip(before, gp))])
     np.savez(os.path.join(out, "rccl.npz"), **rec)
     dist.destroy_process_group()
 
@@ -152,6 +159,7 @@ def test_rccl_single_rank_transport_bit_exact():
     assert rec["t125_equal"][0]
     assert rec["bf16_equal"][0]
     assert rec["gradsync_equal"][0]
+    assert rec["gradsync_a2a_equal"][0]
     for s in (1, 2):
         assert rec[f"sh_theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
         assert rec[f"sh_buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes()
