@@ -866,9 +866,10 @@ def dropin_overlap(spec, dev, ws, rank, cycles, inner_ms=50.0):
     return out
 
 
-def gradsync_rate(spec, dev, ws, rank, steps):
+def gradsync_rate(spec, dev, ws, rank, steps, exchange="rccl"):
     """Per-step DP gradient average of device grads (src/train.py:249-251,
-    src/comm.py:117-123): dl_gather -> RCCL all_reduce -> dl_unpack_avg, pipelined buckets."""
+    src/comm.py:117-123): dl_gather -> RCCL all_reduce -> dl_unpack_avg, pipelined buckets
+    (exchange="a2a": all_to_all -> rank-order average -> all_gather -> copy back)."""
     from diloco_amd.gradsync import GradSync
 
     shapes = [s for _, s in spec.params()]
@@ -877,7 +878,7 @@ def gradsync_rate(spec, dev, ws, rank, steps):
     for i, p in enumerate(params):
         p.grad = torch.empty_like(p)
         synth.fill_device(p.grad.view(-1), synth.noise_seed(9, rank), i, 0.0, 1e-3)
-    gs = GradSync(params, None, ws)
+    gs = GradSync(params, None, ws, exchange=exchange)
     gs.sync()
     _sync(ws)
     t0 = time.perf_counter()
@@ -889,7 +890,8 @@ def gradsync_rate(spec, dev, ws, rank, steps):
     gs.close()
     return {"tree": spec.name, "value": round(4.0 * P / dt / 1e9, 2), "unit": "GB/s",
             "value_aggregate": round(ws * 4.0 * P / dt / 1e9, 2),
-            "ms_per_step": round(dt * 1e3, 4), "buckets": gs.tree.n_buckets}
+            "ms_per_step": round(dt * 1e3, 4), "buckets": gs.tree.n_buckets,
+            "exchange": exchange}
 
 
 def p2p_rate(spec, dev, ws, rank, steps):
@@ -1430,6 +1432,8 @@ def main():
                 False, False, True, "a2a")
             leg(f"{spec.name}_dp_grad_sync", gradsync_rate, spec, dev, ws, rank,
                 max(3, a.steps // 2), brief=False)
+            leg(f"{spec.name}_dp_grad_sync_a2a", gradsync_rate, spec, dev, ws, rank,
+                max(3, a.steps // 2), "a2a", brief=False)
             if ws >= 4 and ws % 2 == 0:  # two concurrent disjoint DP groups (S = 2)
                 leg(f"{spec.name}_two_stages", run_two_stages, spec, dev, ws, rank, a.steps,
                     a.warmup, cap, brief=False)
