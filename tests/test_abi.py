@@ -91,6 +91,24 @@ def test_device_entry_points_fail_loudly_without_gpu():
         _lib.call("dl_sys_fence", None)
     with pytest.raises(_lib.DilocoHipError):
         _lib.call("dl_shard_sgd", 16, _lib.DL_F32, 1, 32, 48, 4, 0.7, 0.9, 1, 0, None)
+    with pytest.raises(_lib.DilocoHipError):
+        _lib.call("dl_shard_reduce_sgd", 16, _lib.DL_F32, 2, 4, 32, 48, 0.7, 0.9, 1, 0, None)
+    with pytest.raises(_lib.DilocoHipError):
+        _lib.call("dl_shard_reduce_avg", 16, _lib.DL_BF16, 3, 8, 32, None)
+
+
+def test_ordered_reduce_argument_checks():
+    """dl_shard_reduce_sgd / _avg reject bad shapes before touching a device."""
+    for args, msg in [((16, _lib.DL_F32, 2, 6, 32, 48, 0.7, 0.9, 1, 0, None), "multiple of 4"),
+                      ((16, _lib.DL_F32, 0, 8, 32, 48, 0.7, 0.9, 1, 0, None), "n_slices"),
+                      ((16, 7, 2, 8, 32, 48, 0.7, 0.9, 1, 0, None), "wire dtype"),
+                      ((16, _lib.DL_F32, 2, 8, 36, 48, 0.7, 0.9, 1, 0, None), "aligned"),
+                      ((16, _lib.DL_F32, 2, 8, 32, 48, 0.7, 0.0, 1, 0, None), "Nesterov")]:
+        with pytest.raises(_lib.DilocoHipError, match=msg):
+            _lib.call("dl_shard_reduce_sgd", *args)
+    with pytest.raises(_lib.DilocoHipError, match="multiple of 4"):
+        _lib.call("dl_shard_reduce_avg", 16, _lib.DL_F32, 2, 5, 32, None)
+    _lib.call("dl_shard_reduce_avg", 16, _lib.DL_F32, 2, 0, 32, None)  # empty: no error
 
 
 def test_missing_library_is_an_import_error(tmp_path, monkeypatch):
