@@ -347,6 +347,11 @@ constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // dl_gather 1 %, dl_scatter / dl_unpack_avg 7 % faster; at T125 / bucket size the same policy
 // is 2-8 % slower (tools/cold_sweep.py "auto", profiles/r02_cold_sweep_flags_auto_*.json).
 constexpr int32_t kBigLaunchChunks = (1 << 28) / DL_CHUNK_ELEMS;
+// int8 unpack: write-through (sc1) stores below that size -- cold on T125-size launches 4.3 and
+// 5.6 % faster than NT on two boxes, neutral (+0 / +1.4 %) over a whole T1.3B tree, which keeps
+// NT (tools/cold_sweep.py --what q8, profiles/r02_cold_sweep_q8_*.json); the fp32 SGD kernels
+// gain nothing from it (profiles/r02_cold_sweep_wt_*.json)
+constexpr int32_t kAutoUnpackSgdQ8 = DL_TUNE_NT_LOADS | DL_TUNE_WT_STORES;
 enum class Big { keep, nt_stores, nt_stores_2 };
 
 int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who,
@@ -368,7 +373,7 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
   L->grid = t->grid;
   L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
   if (t->flags == DL_TUNE_AUTO && big != Big::keep && L->c1 - L->c0 >= kBigLaunchChunks) {
-    L->flags |= DL_TUNE_NT_STORES;
+    L->flags = (L->flags & ~DL_TUNE_WT_STORES) | DL_TUNE_NT_STORES;
     if (big == Big::nt_stores_2 && L->grid == 0) L->grid = (L->c1 - L->c0 + 1) / 2;
   }
   L->stream = static_cast<hipStream_t>(s);
@@ -760,7 +765,7 @@ DL_API int dl_unpack_sgd_q8(dl_tree_t t, int32_t b, const void* slots, float* ou
                             float lr, float momentum, int32_t nesterov, int32_t first_step,
                             int32_t inner_slot, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd_q8", kAutoUnpackSgd));
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd_q8", kAutoUnpackSgdQ8, Big::nt_stores));
   DL_TRY(check_packed(slots, "dl_unpack_sgd_q8", "slots"));
   DL_TRY(check_packed(outer, "dl_unpack_sgd_q8", "outer"));
   if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_unpack_sgd_q8", "momentum"));

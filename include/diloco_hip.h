@@ -104,8 +104,10 @@ DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, 
  * DL_TUNE_WT_STORES | DL_TUNE_REVERSE selects non-temporal loads / non-temporal stores /
  * write-through stores (sc1; wins over NT_STORES; the int8 encoder's payload stays NT) / a
  * last-to-first chunk order for every kernel, DL_TUNE_AUTO (the default) the measured
- * per-kernel choice (NT loads everywhere, NT stores in dl_unpack_sgd). Results are
- * identical for every setting; only speed differs. */
+ * per-kernel choice (NT loads everywhere; NT stores in the SGD kernels and, over launches of
+ * more than 2^28 elements, in dl_delta_pack / dl_gather / dl_scatter / dl_unpack_avg;
+ * write-through stores in dl_unpack_sgd_q8 below that size). Results are identical for
+ * every setting; only speed differs. */
 #define DL_TUNE_NT_LOADS 1
 #define DL_TUNE_NT_STORES 2
 #define DL_TUNE_REVERSE 4 /* walk chunks last to first */

@@ -155,7 +155,8 @@ def main():
                 "q8_reduce": (red, 2 * slot_bytes),
                 "unpack_sgd_q8": (unpack, slot_bytes + 20 * P)}
         shapes = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (1, half): "nt_loads,2chunks/wg",
-                  (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores"}
+                  (3, half): "nt_loads+stores,2chunks/wg",
+                  (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores", (_lib.TUNE_AUTO, 0): "auto"}
         res = {(k, f): [] for k in kern for f in shapes}
         for _ in range(a.rounds):
             for (k, f) in res:
