@@ -336,7 +336,6 @@ namespace {
 
 // per-kernel launch policy under DL_TUNE_AUTO (tools/sweep.py on T125 / T1.3B)
 constexpr int32_t kAutoDelta = DL_TUNE_NT_LOADS;
-constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 constexpr int32_t kAutoOther = DL_TUNE_NT_LOADS;
 // int8 encoder: its one 16-B payload store per lane non-temporal (tools/q8_layout.hip)
 constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
@@ -347,11 +346,17 @@ constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // dl_gather 1 %, dl_scatter / dl_unpack_avg 7 % faster; at T125 / bucket size the same policy
 // is 2-8 % slower (tools/cold_sweep.py "auto", profiles/r02_cold_sweep_flags_auto_*.json).
 constexpr int32_t kBigLaunchChunks = (1 << 28) / DL_CHUNK_ELEMS;
-// int8 unpack: write-through (sc1) stores below that size -- cold on T125-size launches 4.3 and
-// 5.6 % faster than NT on two boxes, neutral (+0 / +1.4 %) over a whole T1.3B tree, which keeps
-// NT (tools/cold_sweep.py --what q8, profiles/r02_cold_sweep_q8_*.json); the fp32 SGD kernels
-// gain nothing from it (profiles/r02_cold_sweep_wt_*.json)
-constexpr int32_t kAutoUnpackSgdQ8 = DL_TUNE_NT_LOADS | DL_TUNE_WT_STORES;
+constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
+// Write-through (sc1) stores: cold, on T125-size launches, 0.5-4.0 % faster than the NT /
+// plain policy in 13 of 14 fp32 kernel-box pairs and 2.2-5.6 % for dl_unpack_sgd_q8 on three
+// boxes; 0.3-3.0 % slower over a whole T1.3B tree (tools/cold_sweep.py,
+// profiles/r02_cold_sweep_wt_*.json, r02_cold_sweep_q8_*.json). But a line stored
+// write-through is not there for the next step to re-read: with the SGD kernels write-through
+// the back-to-back (warm) T125 step fell from ~0.59 to 0.63 ms and the bench line to 785 GB/s
+// while the cold step gained ~1 % (profiles/r02_bench_n1_wt_auto.json,
+// r02_cold_sweep_autowt_*.json). So AUTO keeps NT / plain stores for the fp32 kernels and uses
+// write-through only for the int8 unpack below 2^28 elements.
+constexpr int32_t kAutoWT = DL_TUNE_NT_LOADS | DL_TUNE_WT_STORES;
 enum class Big { keep, nt_stores, nt_stores_2 };
 
 int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who,
@@ -373,7 +378,7 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
   L->grid = t->grid;
   L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
   if (t->flags == DL_TUNE_AUTO && big != Big::keep && L->c1 - L->c0 >= kBigLaunchChunks) {
-    L->flags = (L->flags & ~DL_TUNE_WT_STORES) | DL_TUNE_NT_STORES;
+    L->flags = (L->flags & ~DL_TUNE_WT_STORES) | DL_TUNE_NT_STORES;  // WT -> NT above 2^28
     if (big == Big::nt_stores_2 && L->grid == 0) L->grid = (L->c1 - L->c0 + 1) / 2;
   }
   L->stream = static_cast<hipStream_t>(s);
@@ -765,7 +770,7 @@ DL_API int dl_unpack_sgd_q8(dl_tree_t t, int32_t b, const void* slots, float* ou
                             float lr, float momentum, int32_t nesterov, int32_t first_step,
                             int32_t inner_slot, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd_q8", kAutoUnpackSgdQ8, Big::nt_stores));
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd_q8", kAutoWT, Big::nt_stores));
   DL_TRY(check_packed(slots, "dl_unpack_sgd_q8", "slots"));
   DL_TRY(check_packed(outer, "dl_unpack_sgd_q8", "outer"));
   if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_unpack_sgd_q8", "momentum"));
