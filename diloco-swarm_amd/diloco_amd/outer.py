@@ -207,11 +207,9 @@ class OuterSync:
             self.g_shard = None if self.a2a else torch.zeros(off, dtype=wire_dtype, **z)
             self.mom_shard = (torch.zeros(off, dtype=torch.float32, **z)
                               if self.momentum != 0 else None)
-            if self.a2a:
-                # all_to_all landing buffers, one per bucket in flight (the step overlaps the
-                # exchange of bucket b+1 with the reduce of bucket b): n slices of the shard
-                smax = max(self._shard_len(b) for b in range(self.tree.n_buckets))
-                self.a2a_recv = [torch.zeros(n * smax, dtype=wire_dtype, **z) for _ in range(2)]
+            # exchange="a2a": all_to_all landing buffers, made on first use (a one-replica
+            # engine without a process group never exchanges)
+            self.a2a_recv: Optional[List[torch.Tensor]] = None
         if self.xgmi:
             from .xgmi import PeerMap
 
@@ -330,6 +328,12 @@ class OuterSync:
         return not dist.is_initialized() or dist.get_world_size(self.group) != 1
 
     def _a2a_slices(self, bucket: int) -> torch.Tensor:
+        if self.a2a_recv is None:
+            # one buffer per bucket in flight (the step overlaps the exchange of bucket b+1
+            # with the reduce of bucket b): n slices of the largest shard
+            smax = max(self._shard_len(b) for b in range(self.tree.n_buckets))
+            self.a2a_recv = [torch.zeros(self.world_size * smax, dtype=self.wire_dtype,
+                                         device=self.device) for _ in range(2)]
         return self.a2a_recv[bucket % 2][:self.world_size * self._shard_len(bucket)]
 
     def reduce_scatter(self, bucket: int, async_op: bool = True):
