@@ -672,12 +672,16 @@ hipError_t launch_shard_sgd(const void* wire, int wire_dtype, int divisor, float
 // rank whatever the transport -- then dl_shard_sgd's SGD on this peer's θ and momentum shards.
 // Reads n·sizeof(W) + 8 B, writes 8 B per shard element. N = 0: n read at run time (n > 8).
 // MODE 3 (dl_shard_reduce_avg, the ordered DP gradient sync): no SGD -- `th` receives g.
-constexpr int kSU = 2;                          // float4 rows per lane
-constexpr int64_t kSliceStep = kThreads * kSU * 4;  // 2048 elements per workgroup and round
+// float4 rows per lane: 4 (the walker's 16 KiB per stream and workgroup) while the slices'
+// registers allow it, 2 beyond two slices (N = 8: 16 slice float4 + θ, m per lane)
+template <int N>
+constexpr int slice_rows() { return N >= 1 && N <= 2 ? 4 : 2; }
 template <int N, typename W, int MODE>
 __global__ void __launch_bounds__(kThreads)
     k_slices_sgd(const W* __restrict__ slices, int32_t n, int64_t len, float* __restrict__ th,
                  float* __restrict__ mom, SgdArgs a) {
+  constexpr int kSU = slice_rows<N>();
+  constexpr int64_t kSliceStep = kThreads * kSU * 4;
   const int nn = N > 0 ? N : n;
   for (int64_t base = int64_t(blockIdx.x) * kSliceStep; base < len;
        base += int64_t(gridDim.x) * kSliceStep) {
@@ -743,7 +747,8 @@ __global__ void __launch_bounds__(kThreads)
 template <int N, typename W>
 static hipError_t slices_sgd_n(const W* w, int32_t n, int64_t len, float* th, float* mom,
                                SgdArgs a, hipStream_t s, bool avg_only) {
-  const int64_t blocks = (len + kSliceStep - 1) / kSliceStep;
+  const int64_t step = kThreads * slice_rows<N>() * 4;
+  const int64_t blocks = (len + step - 1) / step;
   const int32_t grid = int32_t(blocks < (1 << 20) ? blocks : (1 << 20));
   if (avg_only)
     hipLaunchKernelGGL((k_slices_sgd<N, W, 3>), dim3(grid), dim3(kThreads), 0, s, w, n, len, th, mom, a);
