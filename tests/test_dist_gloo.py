@@ -183,6 +183,20 @@ def _worker(rank, world, port, mode, num_stages, out):
             eng.step()
             rec[f"theta_s{s}"] = np.concatenate([t.numpy().reshape(-1) for t in eng.unpacked(eng.theta)])
             rec[f"inner_s{s}"] = np.concatenate([p.numpy().reshape(-1) for p in params])
+    elif mode == "dpsync_a2a":
+        # TrainingComm.sync_gradients on a plain-DP model (device grads under the oracle
+        # backend) with DILOCO_DP_EXCHANGE=a2a: the ordered GradSync behind the reference call
+        import diloco_amd.comm as comm_mod
+
+        comm_mod.DP_EXCHANGE = "a2a"
+        g = torch.Generator().manual_seed(100 + rank)
+        m = torch.nn.Module()
+        m.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(n))
+                                       for n in (1, 3, 5000, 64, 4097)])
+        for p in m.parameters():
+            p.grad = torch.randn(p.numel(), generator=g)
+        TrainingComm(world_, (1, 1, 4), None).sync_gradients(m)
+        rec["got"] = np.concatenate([p.grad.numpy() for p in m.parameters()])
     elif mode in ("gradsync", "gradsync_a2a"):
         from diloco_amd.gradsync import GradSync
 
@@ -412,3 +426,6 @@ def test_gradsync_a2a_is_bit_exact_against_rank_order_oracle(world):
     want = oracle.sum_avg(grads)
     for rec in _run("gradsync_a2a", world):
         assert rec["got"].tobytes() == want.tobytes()
+    if world == 4:  # the same through TrainingComm.sync_gradients (DILOCO_DP_EXCHANGE=a2a)
+        for rec in _run("dpsync_a2a", world):
+            assert rec["got"].tobytes() == want.tobytes()
