@@ -7,7 +7,9 @@ tests/test_rccl_gpu.py at one rank and in bench.py at N > 1):
     config #4  fp32 wire, bucketed: delta_pack(b) -> Σ_r wire_r(b) -> unpack_sgd(b), n = 2;
                the sharded default at DP = 8: delta_pack(b) -> reduce-scatter (Σ, slice r)
                -> dl_shard_sgd -> all-gather -> dl_scatter, n = 8
-    config #5  bf16 wire (in-kernel cast) + SGD fused into the unpack, n = 2 and n = 8
+    config #5  bf16 wire (in-kernel cast) + SGD fused into the unpack, n = 2 and n = 8; and
+               with the ordered exchange (exchange="a2a": all_to_all, the n bf16 slices summed
+               in fp32 in rank order, never re-rounded), n = 8
 Expected values come from the C oracle (oracle/diloco_oracle.c) on sampled tensors -- wte
 (103 M elements; a 4 Mi-element window at n = 8), the first block's tensors and the last
 tensor -- restated per slice from the counter-based inputs (every step is elementwise), 2
@@ -70,7 +72,14 @@ def _expected(n, wire, full_wte):
         th32 = th.copy()
         buf, buf32 = np.empty_like(th), np.empty_like(th)
         for s in range(1, STEPS + 1):
-            if wire == "bf16":
+            if wire == "bf16_a2a":
+                # exchange="a2a": deltas cast RNE, summed in fp32 in rank order, / n
+                g = oracle.sum_avg([oracle.bf16_round(oracle.delta(th, x))
+                                    for x in _slice_inputs(t, lo, m, s, n, th)])
+                g32 = oracle.sum_avg([oracle.delta(th32, x)
+                                      for x in _slice_inputs(t, lo, m, s, n, th32)])
+                oracle.sgd(th32, buf32, g32, 0.7, 0.9, True, s == 1)
+            elif wire == "bf16":
                 # the bf16 wire: deltas cast RNE, partial sums rounded to bf16 (RCCL's bf16
                 # reduction, rank order), then g = sum / n in fp32 inside dl_unpack_sgd
                 d = [oracle.bf16_round(oracle.delta(th, x))
@@ -91,12 +100,13 @@ def _expected(n, wire, full_wte):
     return exp
 
 
-def _replicas(n, wire=torch.float32, shard=False):
+def _replicas(n, wire=torch.float32, shard=False, exchange="rccl"):
     shapes = [s for _, s in SPEC.params()]
     engines, inners = [], []
     for r in range(n):
         inner = [t.view(s) for t, s in zip(synth.outer_tree_device(SPEC, DEV), shapes)]
-        engines.append(OuterSync(inner, world_size=n, wire_dtype=wire, shard=shard, rank=r))
+        engines.append(OuterSync(inner, world_size=n, wire_dtype=wire, shard=shard, rank=r,
+                                 exchange=exchange))
         inners.append(inner)
     assert engines[0].tree.n_buckets == 25
     return engines, inners
@@ -151,6 +161,31 @@ def _sharded_step(engines, inners, step):
     torch.cuda.synchronize()
 
 
+def _a2a_step(engines, inners, step):
+    """exchange="a2a": delta_pack(b) -> all_to_all (peer r gets slice r of every rank's wire,
+    in rank order) -> dl_shard_reduce_sgd -> all-gather -> dl_scatter."""
+    _set_inner(engines, inners, step)
+    e0 = engines[0]
+    for b in range(e0.tree.n_buckets):
+        for e in engines:
+            e.pseudo_gradient(b)
+        sl = e0._shard_len(b)
+        for r, e in enumerate(engines):
+            recv = e._a2a_slices(b)
+            for q, src in enumerate(engines):
+                recv[q * sl:(q + 1) * sl].copy_(src.bucket_view(b)[r * sl:(r + 1) * sl])
+            e.shard_apply(b)
+        gathered = torch.cat([e.th_shard_view(b) for e in engines])
+        lo, hi = e0.tree.bucket_ranges[b]
+        for e in engines:
+            e.theta[lo:hi].copy_(gathered)
+            e.write_inner(b)
+        del gathered
+    for e in engines:
+        e.steps_done += 1
+    torch.cuda.synchronize()
+
+
 def _check(engines, inners, exp, step, n, full_wte, wire, sharded=False):
     e0 = engines[0]
     mom_full = e0.momentum_full() if not sharded else None
@@ -167,7 +202,7 @@ def _check(engines, inners, exp, step, n, full_wte, wire, sharded=False):
             assert got.tobytes() == th_exp.tobytes(), (t, lo, step)
             assert inner[t].reshape(-1)[lo:lo + m].cpu().numpy().tobytes() == th_exp.tobytes()
         assert mom_full[o:o + m].cpu().numpy().tobytes() == buf_exp.tobytes(), (t, step)
-        if wire == "bf16":  # the codec's error on the applied update, vs the fp32 oracle
+        if wire.startswith("bf16"):  # the codec's error on the applied update, vs fp32
             th0 = exp[(t, lo, step - 1)][0] if step > 1 else None
             if th0 is not None:
                 u_bf, u_32 = th0 - th_exp, exp[(t, lo, step - 1)][2] - th32
@@ -180,6 +215,8 @@ def _check(engines, inners, exp, step, n, full_wte, wire, sharded=False):
             worst = max(worst, float(np.abs(u_bf - u_32).max()) / scale)
     if wire == "bf16":
         assert worst <= n * 2.0 ** -8, worst
+    elif wire == "bf16_a2a":  # one rounding of each delta, none of the sum: independent of n
+        assert worst <= 2.0 ** -8, worst
     # every replica holds the same full state (a size-independent property over all 1.3 B)
     for e in engines[1:]:
         assert torch.equal(e.theta, e0.theta)
@@ -221,5 +258,19 @@ def test_t13b_eight_replicas_bf16_wire():
     for s in range(1, STEPS + 1):
         _replicated_step(engines, inners, s)
         _check(engines, inners, exp, s, 8, False, "bf16")
+    for e in engines:
+        e.close()
+
+
+def test_t13b_eight_replicas_bf16_wire_ordered_exchange():
+    """Config #5 at DP = 8 with exchange="a2a": the bf16 slices of every replica summed in fp32
+    in rank order by dl_shard_reduce_sgd (SGD on the shard), all-gather, scatter; bit-exact
+    against the oracle's restatement, within 2^-8 of the fp32 oracle at any n."""
+    exp = _expected(8, "bf16_a2a", full_wte=False)
+    engines, inners = _replicas(8, torch.bfloat16, shard=None, exchange="a2a")
+    assert engines[0].sharded and engines[0].a2a
+    for s in range(1, STEPS + 1):
+        _a2a_step(engines, inners, s)
+        _check(engines, inners, exp, s, 8, False, "bf16_a2a", sharded=True)
     for e in engines:
         e.close()
