@@ -751,14 +751,24 @@ def parity_q8(dev, ws, rank):
             "replicas_identical": identical, "ok": bool(worst <= 1.0 and identical)}
 
 
-def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync", inner_fn=None):
+# HBM bytes per parameter of the device drop-in sequence (placement="device"), by (fused, N>1):
+# fused one peer: dl_delta_pack_sgd (read θ, inner, m; write wire, θ, m, inner); fused N > 1:
+# dl_delta_pack (12) before each bucket's all_reduce + dl_unpack_sgd with the /n and the inner
+# write (24); eager: dl_delta_pack 12 + (dl_unpack_avg 8) + dl_unpack_sgd 20 + dl_scatter 8
+DROPIN_DEVICE_BPP = {(True, False): 28, (True, True): 36, (False, False): 40, (False, True): 48}
+
+
+def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync", inner_fn=None,
+                fused=None):
     """The reference's call sequence (src/train.py:261-269) through the drop-in functions.
     placement "host": the reference's host-resident outer model, PCIe transfers included
-    (DESIGN.md "Host-memory ends"); "device": the outer model in HBM.
+    (DESIGN.md "Host-memory ends"); "device": the outer model in HBM,
+    fused (default: DILOCO_OUTER_FUSED, on) or eager (fused=False; mirror.DeviceOuterMirror).
     write_back "deferred": the host placement's write-back DMAs issued by sync_inner_model
     and not waited for. inner_fn: GPU work standing in for the inner steps that follow an
     outer step in training, enqueued after it and inside the timed cycle (the reference
-    synchronises the device after every inner step, src/train.py:243)."""
+    synchronises the device after every inner step, src/train.py:243). Each cycle ends with a
+    device synchronize, so the host work of the four calls is inside the time."""
     from types import SimpleNamespace
 
     from diloco_amd.comm import TrainingComm
@@ -775,7 +785,8 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync",
     inner = torch.nn.Module()
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
-    outer = get_outer_model(inner, placement, write_back=write_back)
+    outer = get_outer_model(inner, placement, write_back=write_back, fused=fused)
+    is_fused = bool(getattr(outer, "_diloco_fused", False))
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
@@ -813,15 +824,41 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync",
         d2h = (16 if ws > 1 and write_back == "sync" else 12) * P
     if inner_fn is not None:
         phases["inner_work_and_sync"] = phases.pop("sync_inner_model")
-    return {"tree": spec.name, "value": round(4.0 * P / dt / 1e9, 2), "unit": "GB/s",
-            "value_aggregate": round(ws * 4.0 * P / dt / 1e9, 2),
-            "ms_per_step": round(dt * 1e3, 3),
-            "phase_ms": {k: round(v / steps * 1e3, 3) for k, v in phases.items()},
-            "placement": placement, "write_back": write_back,
-            "d2h_bytes_per_step": d2h,
-            "note": ("host outer model (reference semantics); D2H of delta, (avg,) θ, momentum"
-                     if placement == "host" else
-                     "outer model in HBM (params/.grad/momentum are packed views); no PCIe")}
+    res = {"tree": spec.name, "value": round(4.0 * P / dt / 1e9, 2), "unit": "GB/s",
+           "value_aggregate": round(ws * 4.0 * P / dt / 1e9, 2),
+           "ms_per_step": round(dt * 1e3, 3),
+           "phase_ms": {k: round(v / steps * 1e3, 3) for k, v in phases.items()},
+           "placement": placement, "write_back": write_back,
+           "d2h_bytes_per_step": d2h,
+           "note": ("host outer model (reference semantics); D2H of delta, (avg,) θ, momentum"
+                    if placement == "host" else
+                    "outer model in HBM (params/.grad/momentum are packed views); no PCIe")}
+    if placement == "device" and inner_fn is None:
+        # the GPU span of the four calls (events on the stream they launch on, around each
+        # cycle; no synchronize inside): at one peer and fused, the one dl_delta_pack_sgd
+        bpp = DROPIN_DEVICE_BPP[(is_fused, ws > 1)]
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+        for e in ev:
+            e[0].record()
+            compute_pseudo_gradient(inner, outer)
+            comm.sync_gradients(outer)
+            opt.step()
+            sync_inner_model(outer, inner)
+            e[1].record()
+        torch.cuda.synchronize()
+        span = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+        res.update(fused=is_fused, hbm_bytes_per_param=bpp, gpu_span_ms=round(span, 5),
+                   kernels_launched=("dl_delta_pack_sgd" if is_fused and ws == 1 else
+                                     "dl_delta_pack / all_reduce / dl_unpack_sgd(+inner)"
+                                     if is_fused else
+                                     "dl_delta_pack / (all_reduce + dl_unpack_avg) / "
+                                     "dl_unpack_sgd / dl_scatter"))
+        if ws == 1:
+            name = "delta_pack_sgd" if is_fused else "dropin_eager_sequence"
+            res["roofline"] = dict(kernel_entry(bpp * P, span), kernel=name)
+        # the values the calls leave behind equal the engine's one-pass step (bit-exact):
+        # checked by tests/test_dropin_gpu.py at T125 against the C oracle
+    return res
 
 
 def dropin_overlap(spec, dev, ws, rank, cycles, inner_ms=50.0):
@@ -1450,6 +1487,8 @@ def main():
                                          into={}, brief=False)
             leg(f"{spec.name}_dropin_device", dropin_rate, spec, dev, ws, rank, 10, "device",
                 brief=False)
+            leg(f"{spec.name}_dropin_device_eager", dropin_rate, spec, dev, ws, rank, 10,
+                "device", "sync", None, False, brief=False)
             leg(f"{spec.name}_dropin_overlap", dropin_overlap, spec, dev, ws, rank, 5,
                 brief=False)
         if ws == 1 and not a.no_cpu_baseline:

@@ -71,6 +71,12 @@ namespace dl {
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 }  // namespace dl
 
+struct dl_tree_s;
+namespace {
+int slot_begin(dl_tree_s* t, int32_t slot, hipStream_t s, const char* who);
+int slot_end(dl_tree_s* t, int32_t slot, hipStream_t s, const char* who);
+}  // namespace
+
 // Pointer-table uploads go through a small ring of pinned staging slots, each guarded by the
 // event of the copy that last read it, so dl_tree_bind never synchronises the host with the
 // stream (a DP sync rebinding reallocated .grad tensors every inner step stays asynchronous).
@@ -96,8 +102,33 @@ struct dl_tree_s {
   std::vector<uint8_t> slot_aligned;
   int32_t grid = 0;                 // 0 = one workgroup per chunk
   int32_t flags = DL_TUNE_AUTO;
-  int32_t slot_period = 0, slot_read = 0;  // dl_tree_slot (0 = off)
+  // Per slot: the event recorded after its last bind or launch and that call's stream. A bind
+  // or launch on another stream waits for it first, so the slot's address table is never
+  // rewritten under (or read before) work queued on a stream the caller did not order.
+  hipEvent_t slot_ev[DL_MAX_SLOTS] = {};
+  hipStream_t slot_stream[DL_MAX_SLOTS] = {};
+  bool slot_used[DL_MAX_SLOTS] = {};
 };
+
+namespace {
+// Cross-stream ordering of a slot (dl_tree_s::slot_ev): a bind or launch that uses `slot` on a
+// stream other than the slot's last one first waits for the event recorded after that use;
+// every use records the event again afterwards. One stream (the usual case) costs one event
+// record per call and no wait.
+int slot_begin(dl_tree_s* t, int32_t slot, hipStream_t s, const char* who) {
+  if (slot < 0) return DL_OK;
+  if (t->slot_used[slot] && t->slot_stream[slot] != s)
+    DL_HIP(hipStreamWaitEvent(s, t->slot_ev[slot], 0), who);
+  return DL_OK;
+}
+int slot_end(dl_tree_s* t, int32_t slot, hipStream_t s, const char* who) {
+  if (slot < 0) return DL_OK;
+  DL_HIP(hipEventRecord(t->slot_ev[slot], s), who);
+  t->slot_stream[slot] = s;
+  t->slot_used[slot] = true;
+  return DL_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -194,6 +225,8 @@ DL_API int dl_tree_create_ex(const int64_t* numel, int32_t n, int64_t cap_elems,
                       hipHostMallocDefault);
   for (int i = 0; i < kStageRing && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&t->stage_ev[i], hipEventDisableTiming);
+  for (int i = 0; i < DL_MAX_SLOTS && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&t->slot_ev[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     int rc2 = hip_fail(e, "dl_tree_create");
     dl_tree_destroy(t);
@@ -211,6 +244,8 @@ DL_API int dl_tree_destroy(dl_tree_t t) {
       if (t->stage_used[i]) (void)hipEventSynchronize(t->stage_ev[i]);
       (void)hipEventDestroy(t->stage_ev[i]);
     }
+  for (int i = 0; i < DL_MAX_SLOTS; ++i)
+    if (t->slot_ev[i]) (void)hipEventDestroy(t->slot_ev[i]);
   if (t->d_chunks) (void)hipFree(t->d_chunks);
   if (t->d_loff) (void)hipFree(t->d_loff);
   if (t->d_caddr) (void)hipFree(t->d_caddr);
@@ -266,23 +301,26 @@ DL_API int dl_tree_bucket_chunks(dl_tree_t t, int32_t b, int32_t* c0, int32_t* c
 
 DL_API int dl_tree_tune(dl_tree_t t, int32_t max_blocks, int32_t flags) {
   if (!t || max_blocks < 0) return fail(DL_E_ARG, "dl_tree_tune: bad argument");
-  if (flags != DL_TUNE_AUTO &&
-      (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES | DL_TUNE_WT_STORES | DL_TUNE_REVERSE)))
+  if (flags != DL_TUNE_AUTO && (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES | DL_TUNE_WT_STORES)))
     return fail(DL_E_ARG, "dl_tree_tune: unknown flags 0x%x", flags);
+#ifndef DL_TUNING
+  // the product build instantiates the AUTO policies only: NT loads, plain or NT stores
+  if (flags != DL_TUNE_AUTO && (!(flags & DL_TUNE_NT_LOADS) || (flags & DL_TUNE_WT_STORES)))
+    return fail(DL_E_ARG,
+                "dl_tree_tune: flags 0x%x need the tuning build (make TUNING=1): the product "
+                "library has NT loads with plain or NT stores only", flags);
+#endif
   t->grid = max_blocks;
   t->flags = flags;
   return DL_OK;
 }
 
-DL_API int dl_tree_slot(dl_tree_t t, int32_t period_ticks, int32_t read_ticks) {
-  if (!t) return fail(DL_E_ARG, "dl_tree_slot: null tree");
-  if (period_ticks < 0 || read_ticks < 0 || (period_ticks > 0 && read_ticks >= period_ticks) ||
-      period_ticks > 1000000)
-    return fail(DL_E_ARG, "dl_tree_slot: period %d, read %d ticks (0 <= read < period <= 10^6)",
-                period_ticks, read_ticks);
-  t->slot_period = period_ticks;
-  t->slot_read = period_ticks > 0 ? read_ticks : 0;
-  return DL_OK;
+DL_API int dl_tuning_build(void) {
+#ifdef DL_TUNING
+  return 1;
+#else
+  return 0;
+#endif
 }
 
 DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t n,
@@ -307,6 +345,8 @@ DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t
   // has not landed), one n-entry copy to the device, then dl_resolve_chunks expands them into
   // the slot's per-chunk address table. Kernels queued earlier on `s` still read the previous
   // table; the rewrite is ordered behind them.
+  const int rc0 = slot_begin(t, slot, s, "dl_tree_bind");
+  if (rc0) return rc0;
   const int k = t->stage_next;
   t->stage_next = (k + 1) % kStageRing;
   if (t->stage_used[k]) {  // normally long landed: a query, a wait only if it has not
@@ -327,7 +367,7 @@ DL_API int dl_tree_bind(dl_tree_t t, int32_t slot, const uint64_t* ptrs, int32_t
                                    t->d_caddr + size_t(slot) * nch, s),
          "dl_tree_bind(resolve)");
   t->bound[slot] = 1;
-  return DL_OK;
+  return slot_end(t, slot, s, "dl_tree_bind");
 }
 
 }  // extern "C"
@@ -382,8 +422,6 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
     if (big == Big::nt_stores_2 && L->grid == 0) L->grid = (L->c1 - L->c0 + 1) / 2;
   }
   L->stream = static_cast<hipStream_t>(s);
-  L->slot_period = t->slot_period;
-  L->slot_read = t->slot_read;
   return DL_OK;
 }
 
@@ -423,8 +461,9 @@ DL_API int dl_delta_pack(dl_tree_t t, int32_t b, int32_t inner_slot, const float
   DL_TRY(check_packed(outer, "dl_delta_pack", "outer"));
   DL_TRY(check_packed(wire, "dl_delta_pack", "wire"));
   DL_TRY(check_dtype(wire_dtype, "dl_delta_pack"));
+  DL_TRY(slot_begin(t, inner_slot, L.stream, "dl_delta_pack"));
   hipError_t e = dl::launch_delta_pack(L, inner_slot, outer, wire, wire_dtype);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_pack");
+  return e == hipSuccess ? slot_end(t, inner_slot, L.stream, "dl_delta_pack") : hip_fail(e, "dl_delta_pack");
 }
 
 DL_API int dl_unpack_avg(dl_tree_t t, int32_t b, const void* wire, int32_t wire_dtype,
@@ -438,8 +477,9 @@ DL_API int dl_unpack_avg(dl_tree_t t, int32_t b, const void* wire, int32_t wire_
     DL_TRY(check_slot(t, dst_slot, "dl_unpack_avg"));
   else
     DL_TRY(check_packed(dst_packed, "dl_unpack_avg", "dst_packed"));
+  DL_TRY(slot_begin(t, dst_slot, L.stream, "dl_unpack_avg"));
   hipError_t e = dl::launch_unpack_avg(L, wire, wire_dtype, divisor, dst_slot, dst_packed);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_unpack_avg");
+  return e == hipSuccess ? slot_end(t, dst_slot, L.stream, "dl_unpack_avg") : hip_fail(e, "dl_unpack_avg");
 }
 
 DL_API int dl_unpack_sgd(dl_tree_t t, int32_t b, const void* wire, int32_t wire_dtype,
@@ -457,8 +497,9 @@ DL_API int dl_unpack_sgd(dl_tree_t t, int32_t b, const void* wire, int32_t wire_
   if (nesterov && momentum == 0.f)
     return fail(DL_E_ARG, "dl_unpack_sgd: Nesterov momentum requires a momentum");
   dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  DL_TRY(slot_begin(t, inner_slot, L.stream, "dl_unpack_sgd"));
   hipError_t e = dl::launch_unpack_sgd(L, wire, wire_dtype, divisor, outer, mom, a, inner_slot);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_unpack_sgd");
+  return e == hipSuccess ? slot_end(t, inner_slot, L.stream, "dl_unpack_sgd") : hip_fail(e, "dl_unpack_sgd");
 }
 
 DL_API int dl_delta_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer, float* mom,
@@ -472,8 +513,9 @@ DL_API int dl_delta_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer
   if (nesterov && momentum == 0.f)
     return fail(DL_E_ARG, "dl_delta_sgd: Nesterov momentum requires a momentum");
   dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  DL_TRY(slot_begin(t, inner_slot, L.stream, "dl_delta_sgd"));
   hipError_t e = dl::launch_delta_sgd(L, inner_slot, outer, mom, a);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_sgd");
+  return e == hipSuccess ? slot_end(t, inner_slot, L.stream, "dl_delta_sgd") : hip_fail(e, "dl_delta_sgd");
 }
 
 DL_API int dl_delta_pack_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* outer, void* wire,
@@ -489,8 +531,9 @@ DL_API int dl_delta_pack_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* 
   if (nesterov && momentum == 0.f)
     return fail(DL_E_ARG, "dl_delta_pack_sgd: Nesterov momentum requires a momentum");
   dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  DL_TRY(slot_begin(t, inner_slot, L.stream, "dl_delta_pack_sgd"));
   hipError_t e = dl::launch_delta_pack_sgd(L, inner_slot, outer, wire, wire_dtype, mom, a);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_pack_sgd");
+  return e == hipSuccess ? slot_end(t, inner_slot, L.stream, "dl_delta_pack_sgd") : hip_fail(e, "dl_delta_pack_sgd");
 }
 
 // a2 -> (one peer: the exchange is the identity, src/comm.py:118-119) -> a3-a5, cache-blocked:
@@ -514,6 +557,7 @@ DL_API int dl_pack_sgd_tiled(dl_tree_t t, int32_t b, int32_t inner_slot, float* 
     return fail(DL_E_ARG, "dl_pack_sgd_tiled: Nesterov momentum requires a momentum");
   if (tile_chunks < 0) return fail(DL_E_ARG, "dl_pack_sgd_tiled: tile_chunks %d", tile_chunks);
   const dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  DL_TRY(slot_begin(t, inner_slot, P.stream, "dl_pack_sgd_tiled"));
   const int32_t c0 = P.c0, c1 = P.c1;
   const int32_t step = tile_chunks > 0 ? tile_chunks : (c1 - c0 > 0 ? c1 - c0 : 1);
   for (int32_t c = c0; c < c1; c += step) {
@@ -525,7 +569,7 @@ DL_API int dl_pack_sgd_tiled(dl_tree_t t, int32_t b, int32_t inner_slot, float* 
       err = dl::launch_unpack_sgd(U, wire, wire_dtype, 1, outer, mom, a, inner_slot);
     if (err != hipSuccess) return hip_fail(err, "dl_pack_sgd_tiled");
   }
-  return DL_OK;
+  return slot_end(t, inner_slot, P.stream, "dl_pack_sgd_tiled");
 }
 
 DL_API int dl_shard_sgd(const void* wire, int32_t wire_dtype, int32_t divisor, float* outer,
@@ -751,8 +795,9 @@ DL_API int dl_delta_q8(dl_tree_t t, int32_t b, int32_t inner_slot, const float* 
   DL_TRY(check_slot(t, inner_slot, "dl_delta_q8"));
   DL_TRY(check_packed(outer, "dl_delta_q8", "outer"));
   DL_TRY(check_packed(slots, "dl_delta_q8", "slots"));
+  DL_TRY(slot_begin(t, inner_slot, L.stream, "dl_delta_q8"));
   hipError_t e = dl::launch_delta_q8(L, inner_slot, outer, static_cast<uint8_t*>(slots));
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_delta_q8");
+  return e == hipSuccess ? slot_end(t, inner_slot, L.stream, "dl_delta_q8") : hip_fail(e, "dl_delta_q8");
 }
 
 DL_API int dl_q8_reduce(const void* recv, int32_t n, int32_t m, int32_t divisor, void* out,
@@ -778,9 +823,11 @@ DL_API int dl_unpack_sgd_q8(dl_tree_t t, int32_t b, const void* slots, float* ou
   if (nesterov && momentum == 0.f)
     return fail(DL_E_ARG, "dl_unpack_sgd_q8: Nesterov momentum requires a momentum");
   dl::SgdArgs a{-lr, momentum, nesterov ? 1 : 0, first_step ? 1 : 0};
+  DL_TRY(slot_begin(t, inner_slot, L.stream, "dl_unpack_sgd_q8"));
   hipError_t e = dl::launch_unpack_sgd_q8(L, static_cast<const uint8_t*>(slots), outer, mom, a,
                                           inner_slot);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_unpack_sgd_q8");
+  return e == hipSuccess ? slot_end(t, inner_slot, L.stream, "dl_unpack_sgd_q8")
+                         : hip_fail(e, "dl_unpack_sgd_q8");
 }
 
 DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int32_t dtype,
@@ -790,8 +837,9 @@ DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int
   DL_TRY(check_slot(t, src_slot, "dl_gather"));
   DL_TRY(check_packed(packed, "dl_gather", "packed"));
   DL_TRY(check_dtype(dtype, "dl_gather"));
+  DL_TRY(slot_begin(t, src_slot, L.stream, "dl_gather"));
   hipError_t e = dl::launch_gather(L, src_slot, packed, dtype);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_gather");
+  return e == hipSuccess ? slot_end(t, src_slot, L.stream, "dl_gather") : hip_fail(e, "dl_gather");
 }
 
 DL_API int dl_scatter(dl_tree_t t, int32_t b, const float* packed, int32_t dst_slot,
@@ -800,8 +848,9 @@ DL_API int dl_scatter(dl_tree_t t, int32_t b, const float* packed, int32_t dst_s
   DL_TRY(make_launch(t, b, s, &L, "dl_scatter", kAutoOther, Big::nt_stores_2));
   DL_TRY(check_slot(t, dst_slot, "dl_scatter"));
   DL_TRY(check_packed(packed, "dl_scatter", "packed"));
+  DL_TRY(slot_begin(t, dst_slot, L.stream, "dl_scatter"));
   hipError_t e = dl::launch_scatter(L, packed, dst_slot);
-  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_scatter");
+  return e == hipSuccess ? slot_end(t, dst_slot, L.stream, "dl_scatter") : hip_fail(e, "dl_scatter");
 }
 
 DL_API int dl_serialize(const void* src, int32_t src_dtype, int64_t numel, float meta0,
@@ -813,6 +862,15 @@ DL_API int dl_serialize(const void* src, int32_t src_dtype, int64_t numel, float
   hipError_t e = dl::launch_serialize(src, src_dtype, numel, meta0, meta1, out,
                                       static_cast<hipStream_t>(s));
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_serialize");
+}
+
+DL_API int dl_serialize_f64(const double* src, int64_t numel, float meta0, float meta1,
+                            double* out, dl_stream_t s) {
+  if (!src || !out) return fail(DL_E_ARG, "dl_serialize_f64: null pointer");
+  if (numel < 2) return fail(DL_E_ARG, "dl_serialize_f64: numel %lld < 2", (long long)numel);
+  hipError_t e = dl::launch_serialize_f64(src, numel, meta0, meta1, out,
+                                          static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_serialize_f64");
 }
 
 DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id, float base,

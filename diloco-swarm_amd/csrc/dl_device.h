@@ -149,16 +149,17 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 }
 
 // ---- the walker ----------------------------------------------------------------------------
-// Body::run is instantiated per (NTL, NTS) policy: non-temporal loads; plain / NT / WT stores.
-// rev: walk the range last chunk first (workgroups are dispatched in blockIdx order), so a
-// kernel that follows one which streamed the same buffers front to back starts on the bytes
-// most likely still in the Infinity Cache.
+// Body::run is instantiated per (NTL, NTS) policy. The product build instantiates what
+// DL_TUNE_AUTO selects: non-temporal loads with plain or non-temporal stores, and write-through
+// stores for the bodies that declare kWriteThrough (dl_unpack_sgd_q8). `make TUNING=1`
+// (-DDL_TUNING) instantiates the whole matrix -- plain loads, write-through for every body --
+// for the measurement tools (tools/cold_sweep.py); dl_tree_tune rejects the rest otherwise.
 template <class Body, bool NTL, int NTS>
 __global__ void __launch_bounds__(kThreads)
     k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ caddr,
-           int32_t nchunk, int32_t rev, Body body) {
+           int32_t nchunk, Body body) {
   for (int32_t i = int32_t(blockIdx.x); i < c1 - c0; i += int32_t(gridDim.x)) {
-    const int32_t c = rev ? c1 - 1 - i : c0 + i;
+    const int32_t c = c0 + i;
     const Chunk ck = chunks[c];
     body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x));
   }
@@ -176,85 +177,19 @@ __device__ __forceinline__ void sgd1(float g, float& buf, float& th, const SgdAr
   }
 }
 
-// ---- clock-slotted walker (dl_tree_slot) ----------------------------------------------------
-// HBM serves a streaming kernel's reads at ~7 TB/s and its writes at 5.5-6.9, but the steady
-// mix of both that a one-workgroup-per-chunk walker produces runs ~10 % below the time the
-// reads and the writes take separately (tools/rw_mix.hip). The slotted walker
-// separates them in time without any communication between workgroups: a resident grid, each
-// workgroup pacing its rounds by the chip's 100 MHz real-time counter (s_memrealtime) from its
-// own start -- all loads of a round issued at the round's start, all stores `read` ticks
-// later, the next round `period` ticks after the last -- so the whole chip reads, then writes. A workgroup behind schedule goes at once
-// instead of skipping a slot; every wait ends when the counter passes a target at most one
-// period ahead. Results do not depend on the timing (same arithmetic, same stores).
-__device__ __forceinline__ uint64_t rtc() { return __builtin_amdgcn_s_memrealtime(); }
-__device__ __forceinline__ void wait_until(uint64_t t) {
-  while (rtc() < t) __builtin_amdgcn_s_sleep(2);
-  __asm__ volatile("" ::: "memory");
-}
-
-// called by a body between its loads (and arithmetic) and its stores
-struct NoGate {
-  __device__ __forceinline__ void operator()() const {}
-};
-struct SlotGate {
-  uint64_t t;
-  __device__ __forceinline__ void operator()() const {
-    __asm__ volatile("" ::: "memory");
-    wait_until(t);
-  }
-};
-
 template <class Body, bool NTL, int NTS>
-__global__ void __launch_bounds__(kThreads)
-    k_walk_slotted(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1,
-                   void* const* __restrict__ caddr, int32_t nchunk, uint32_t period,
-                   uint32_t read, Body body) {
-  // the first round starts at once: the resident grid is dispatched within a few us, so the
-  // workgroups' own start times already agree to a small fraction of a period
-  uint64_t slot = rtc();
-  for (int32_t i = int32_t(blockIdx.x); i < c1 - c0; i += int32_t(gridDim.x), slot += period) {
-    const int32_t c = c0 + i;
-    const Chunk ck = chunks[c];
-    wait_until(slot);
-    body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x), SlotGate{slot + read});
-  }
-}
-
-// workgroups of k that fit on the device at once (the slotted walker's grid)
-template <class K>
-int32_t resident_grid(K kernel) {
-  int per_cu = 0, cus = 0, dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess)
-    return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
-  return per_cu * cus;
-}
-
-// bodies that take a gate between their loads and their stores declare kSlotted = true
-template <class B, class = void>
-struct slotted : std::false_type {};
-template <class B>
-struct slotted<B, std::void_t<decltype(B::kSlotted)>> : std::bool_constant<B::kSlotted> {};
-
-template <class Body, bool NTL, int NTS>
-hipError_t run_policy(const Launch& L, const Body& body, int32_t grid) {
-  if constexpr (slotted<Body>::value) {
-    if (L.slot_period > 0) {
-      static const int32_t resident = resident_grid(k_walk_slotted<Body, NTL, NTS>);
-      const int32_t n = L.c1 - L.c0;
-      const int32_t g = resident > 0 && resident < n ? resident : n;
-      hipLaunchKernelGGL((k_walk_slotted<Body, NTL, NTS>), dim3(g), dim3(kThreads), 0, L.stream,
-                         L.chunks, L.c0, L.c1, L.caddr, L.nchunk, uint32_t(L.slot_period),
-                         uint32_t(L.slot_read), body);
-      return hipGetLastError();
-    }
-  }
+hipError_t launch_walk(const Launch& L, const Body& body, int32_t grid) {
   hipLaunchKernelGGL((k_walk<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream, L.chunks,
-                     L.c0, L.c1, L.caddr, L.nchunk, (L.flags & DL_TUNE_REVERSE) ? 1 : 0, body);
+                     L.c0, L.c1, L.caddr, L.nchunk, body);
   return hipGetLastError();
 }
+
+// bodies whose AUTO policy stores write-through declare kWriteThrough = true
+template <class B, class = void>
+struct write_through : std::false_type {};
+template <class B>
+struct write_through<B, std::void_t<decltype(B::kWriteThrough)>>
+    : std::bool_constant<B::kWriteThrough> {};
 
 template <class Body>
 hipError_t run(const Launch& L, const Body& body) {
@@ -263,14 +198,22 @@ hipError_t run(const Launch& L, const Body& body) {
   const int32_t grid = (L.grid > 0 && L.grid < n) ? L.grid : n;  // default: one workgroup per chunk
   const bool ntl = (L.flags & DL_TUNE_NT_LOADS) != 0;
   const int sp = (L.flags & DL_TUNE_WT_STORES) ? kStWT : (L.flags & DL_TUNE_NT_STORES) ? kStNT : kStPlain;
-  if (ntl) {
-    if (sp == kStWT) return run_policy<Body, true, kStWT>(L, body, grid);
-    if (sp == kStNT) return run_policy<Body, true, kStNT>(L, body, grid);
-    return run_policy<Body, true, kStPlain>(L, body, grid);
+#ifdef DL_TUNING
+  if (!ntl) {
+    if (sp == kStWT) return launch_walk<Body, false, kStWT>(L, body, grid);
+    if (sp == kStNT) return launch_walk<Body, false, kStNT>(L, body, grid);
+    return launch_walk<Body, false, kStPlain>(L, body, grid);
   }
-  if (sp == kStWT) return run_policy<Body, false, kStWT>(L, body, grid);
-  if (sp == kStNT) return run_policy<Body, false, kStNT>(L, body, grid);
-  return run_policy<Body, false, kStPlain>(L, body, grid);
+  if (sp == kStWT) return launch_walk<Body, true, kStWT>(L, body, grid);
+#else
+  if (!ntl) return hipErrorInvalidValue;  // not instantiated (dl_tree_tune rejects it first)
+  if (sp == kStWT) {
+    if constexpr (write_through<Body>::value) return launch_walk<Body, true, kStWT>(L, body, grid);
+    else return hipErrorInvalidValue;
+  }
+#endif
+  if (sp == kStNT) return launch_walk<Body, true, kStNT>(L, body, grid);
+  return launch_walk<Body, true, kStPlain>(L, body, grid);
 }
 
 }  // namespace

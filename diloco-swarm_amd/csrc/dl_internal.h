@@ -39,10 +39,6 @@ struct Launch {
   int32_t grid;   // 0 = one workgroup per chunk
   int32_t flags;  // DL_TUNE_*
   hipStream_t stream;
-  // clock-slotted launch (dl_tree_slot; 0 = off): a resident grid whose rounds start every
-  // slot_period ticks of the 100 MHz real-time counter, stores slot_read ticks after the loads
-  int32_t slot_period;
-  int32_t slot_read;
 };
 
 // peers of the direct exchange (dl_xgmi.hip): each rank's packed wire and θ, IPC-mapped
@@ -84,6 +80,8 @@ hipError_t launch_q8_reduce(const uint8_t* recv, int32_t n, int32_t m, int32_t d
                             uint8_t* out, hipStream_t s);
 hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype);
 hipError_t launch_scatter(const Launch& L, const float* packed, int dst_slot);
+hipError_t launch_serialize_f64(const double* src, int64_t numel, float m0, float m1, double* out,
+                                hipStream_t s);
 hipError_t launch_serialize(const void* src, int src_dtype, int64_t numel, float m0, float m1,
                             float* out, hipStream_t s);
 hipError_t launch_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id,

@@ -28,10 +28,8 @@ struct DeltaPack {
   int inner_slot;
   const float* outer;
   W* wire;
-  static constexpr bool kSlotted = true;
-  template <bool NTL, int NTS, class G = NoGate>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
-                                      const G& gate = G()) const {
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     const float* in = slot_ptr<const float>(caddr, nchunk, inner_slot, c);
     const float* th = outer + ck.poff;
     W* w = wire + ck.poff;
@@ -46,7 +44,6 @@ struct DeltaPack {
           b[u] = ldf4<NTL>(in, v);
         }
       }
-      gate();
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
@@ -55,7 +52,6 @@ struct DeltaPack {
       const int i = (nv << 2) + tid;
       if (i < ck.len) WireIO<W>::st1(w, i, th[i] - in[i]);
     } else {
-      gate();
       for (int i = tid; i < ck.len; i += kThreads) WireIO<W>::st1(w, i, th[i] - in[i]);
     }
   }
@@ -107,10 +103,8 @@ struct UnpackSgd {
   float d;
   SgdArgs a;
   int inner_slot;
-  static constexpr bool kSlotted = true;
-  template <bool NTL, int NTS, class G = NoGate>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
-                                      const G& gate = G()) const {
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* in = inner_slot >= 0 ? slot_ptr<float>(caddr, nchunk, inner_slot, c) : nullptr;
     const W* w = wire + ck.poff;
     float* th = outer + ck.poff;
@@ -135,7 +129,6 @@ struct UnpackSgd {
         sgd1<MODE>(gg.z, m[u].z, t[u].z, a);
         sgd1<MODE>(gg.w, m[u].w, t[u].w, a);
       }
-      gate();
       store_rows<NTS>(th, t, nv, tid);
       if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
       if (in) store_rows<NTS>(in, t, nv, tid);
@@ -150,7 +143,6 @@ struct UnpackSgd {
         if (in) in[i] = t1;
       }
     } else {
-      gate();
       for (int i = tid; i < ck.len; i += kThreads) {
         float gg = WireIO<W>::ld1(w, i);
         if (DIV) gg = gg / d;
@@ -173,10 +165,8 @@ struct DeltaSgd {
   float* mom;
   SgdArgs a;
   int inner_slot;
-  static constexpr bool kSlotted = true;
-  template <bool NTL, int NTS, class G = NoGate>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
-                                      const G& gate = G()) const {
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
     float* th = outer + ck.poff;
     float* mb = mom + ck.poff;
@@ -200,7 +190,6 @@ struct DeltaSgd {
         sgd1<MODE>(g.z, m[u].z, t[u].z, a);
         sgd1<MODE>(g.w, m[u].w, t[u].w, a);
       }
-      gate();
       store_rows<NTS>(th, t, nv, tid);
       if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
       store_rows<NTS>(in, t, nv, tid);
@@ -214,7 +203,6 @@ struct DeltaSgd {
         in[i] = t1;
       }
     } else {
-      gate();
       for (int i = tid; i < ck.len; i += kThreads) {
         const float g = th[i] - in[i];
         float b = (MODE == 2) ? mb[i] : 0.f, t1 = th[i];
@@ -244,10 +232,8 @@ struct DeltaPackSgd {
     if constexpr (sizeof(W) == 2) return bf2f(f2bf(g));
     else return g;
   }
-  static constexpr bool kSlotted = true;
-  template <bool NTL, int NTS, class G = NoGate>
-  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid,
-                                      const G& gate = G()) const {
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* in = slot_ptr<float>(caddr, nchunk, inner_slot, c);
     float* th = outer + ck.poff;
     float* mb = mom + ck.poff;
@@ -274,7 +260,6 @@ struct DeltaPackSgd {
         sgd1<MODE>(g.z, m[u].z, t[u].z, a);
         sgd1<MODE>(g.w, m[u].w, t[u].w, a);
       }
-      gate();
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
@@ -295,7 +280,6 @@ struct DeltaPackSgd {
         in[i] = t1;
       }
     } else {
-      gate();
       for (int i = tid; i < ck.len; i += kThreads) {
         const float g0 = th[i] - in[i];
         WireIO<W>::st1(w, i, g0);
@@ -412,6 +396,19 @@ __global__ void __launch_bounds__(kThreads)
   const int64_t stride = int64_t(gridDim.x) * kThreads;
   for (int64_t v = int64_t(blockIdx.x) * kThreads + threadIdx.x; v < nv; v += stride)
     dst[v] = src[v];
+}
+
+__global__ void __launch_bounds__(kThreads)
+    k_serialize_f64(const double* __restrict__ src, int64_t numel, float m0, float m1,
+                    double* __restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    out[0] = double(m0);
+    out[1] = double(m1);
+  }
+  double* dst = out + numel;
+  const int64_t stride = int64_t(gridDim.x) * kThreads;
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < numel; i += stride)
+    dst[i] = src[i];
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -839,6 +836,13 @@ hipError_t launch_serialize(const void* src, int src_dtype, int64_t numel, float
     hipLaunchKernelGGL(k_serialize<half_bits>, dim3(grid_for(numel)), dim3(kThreads), 0, s,
                        static_cast<const half_bits*>(src), numel, m0, m1, out);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_serialize_f64(const double* src, int64_t numel, float m0, float m1, double* out,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(k_serialize_f64, dim3(grid_for(numel)), dim3(kThreads), 0, s, src, numel, m0,
+                     m1, out);
   return hipGetLastError();
 }
 

@@ -142,6 +142,7 @@ struct UnpackSgdQ8 {
   float* mom;
   SgdArgs a;
   int inner_slot;
+  static constexpr bool kWriteThrough = true;  // its AUTO policy below 2^28 elements
   template <bool NTL, int NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* in = inner_slot >= 0 ? slot_ptr<float>(caddr, nchunk, inner_slot, c) : nullptr;
@@ -210,8 +211,8 @@ struct UnpackSgdQ8 {
 
 // Σ over n peers' copies of m slots (recv laid out [peer][slot]) -> averaged, re-quantised slots
 __global__ void __launch_bounds__(kThreads)
-    k_q8_reduce(const uint8_t* __restrict__ recv, int32_t n, int32_t m, int32_t divisor,
-                uint8_t* __restrict__ out) {
+    k_q8_reduce(const uint8_t* recv, int32_t n, int32_t m, int32_t divisor,
+                uint8_t* out) {  // recv == out at one peer (in place): no __restrict__
   const int j = blockIdx.x;
   const int tid = threadIdx.x;
   float4 acc[kUnroll];

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get(
 )
 
 # constants mirrored from include/diloco_hip.h
-ABI_VERSION = 1
+ABI_VERSION = 2
 ALIGN_ELEMS = 64
 CHUNK_ELEMS = 4096
 ALL_BUCKETS = -1
@@ -23,7 +23,7 @@ MAX_SLOTS = 4
 Q8_SLOT_BYTES = 4160
 IPC_HANDLE_BYTES = 64
 DL_F32, DL_BF16, DL_F16, DL_U8 = 0, 1, 2, 3
-TUNE_NT_LOADS, TUNE_NT_STORES, TUNE_REVERSE, TUNE_WT_STORES = 1, 2, 4, 8
+TUNE_NT_LOADS, TUNE_NT_STORES, TUNE_WT_STORES = 1, 2, 8
 TUNE_AUTO = -1
 COPY_WIDE, COPY_READ, COPY_WRITE = 8, 16, 32
 
@@ -52,7 +52,7 @@ SIGNATURES = {
     "dl_tree_bucket_chunks": (ctypes.c_int, [_vp, _i32, _pi32, _pi32]),
     "dl_tree_bind": (ctypes.c_int, [_vp, _i32, _pu64, _i32, _vp]),
     "dl_tree_tune": (ctypes.c_int, [_vp, _i32, _i32]),
-    "dl_tree_slot": (ctypes.c_int, [_vp, _i32, _i32]),
+    "dl_tuning_build": (ctypes.c_int, []),
     "dl_delta_pack": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _vp]),
     "dl_unpack_avg": (ctypes.c_int, [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp]),
     "dl_unpack_sgd": (
@@ -82,6 +82,7 @@ SIGNATURES = {
     "dl_gather": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp]),
     "dl_scatter": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp]),
     "dl_serialize": (ctypes.c_int, [_vp, _i32, _i64, _f32, _f32, _vp, _vp]),
+    "dl_serialize_f64": (ctypes.c_int, [_vp, _i64, _f32, _f32, _vp, _vp]),
     "dl_fill_synth": (ctypes.c_int, [_vp, _i64, _u64, _u64, _f32, _f32, _vp, _vp]),
     "dl_rccl_load": (ctypes.c_int, [ctypes.c_char_p]),
     "dl_rccl_version": (ctypes.c_int, [_pi32]),

@@ -41,6 +41,16 @@ class GradSync:
         if exchange not in ("rccl", "a2a"):
             raise ValueError(f"exchange {exchange!r}: 'rccl' or 'a2a'")
         self.a2a = exchange == "a2a"
+        if dist.is_initialized() and self.world_size > 1:
+            gs = dist.get_world_size(group)
+            if gs != self.world_size:  # the collectives would reduce over the wrong ranks
+                raise ValueError(f"GradSync(world_size={self.world_size}) on a process group "
+                                 f"of {gs} ranks")
+        # one replica: the all-reduce is the identity -- with no process group, or a group of
+        # other ranks this replica does not average with (OuterSync._local's rule); a one-rank
+        # group carries it (the single-rank RCCL transport test)
+        self.local = self.world_size == 1 and (
+            not dist.is_initialized() or dist.get_world_size(group) != 1)
         if self.a2a and wire_dtype != torch.float32:
             raise ValueError("GradSync(exchange='a2a') averages the fp32 grads")
         self.numels = [p.numel() for p in self.params]
@@ -88,9 +98,9 @@ class GradSync:
             lo, hi = self.tree.bucket_ranges[b]
             return self.wire[lo:hi]
 
-        # one replica with no process group: the all-reduce is the identity (the rebinding,
-        # gather and /1 still run, so the path is exercised on a one-GPU machine)
-        local = self.world_size == 1 and not dist.is_initialized()
+        # one replica (self.local): the all-reduce is the identity (the rebinding, gather and
+        # /1 still run, so the path is exercised on a one-GPU machine)
+        local = self.local
         if self.a2a and not local:
             self._sync_a2a()
             return

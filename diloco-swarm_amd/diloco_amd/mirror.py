@@ -29,6 +29,8 @@ device copy is newer is an error, not a silent overwrite.
 """
 from __future__ import annotations
 
+import weakref
+from collections import OrderedDict
 from typing import List, Optional, Sequence
 
 import torch
@@ -301,20 +303,99 @@ class HostOuterMirror:
         self.tree.close()
 
 
+
+# The C-level `.grad` of every tensor: the mirror reads and assigns it through this
+# descriptor, bypassing OuterParameter's property (no recursion, no per-access Python call).
+_GRAD = torch._C.TensorBase.grad
+
+
+def _sig(ts: Sequence[torch.Tensor]) -> tuple:
+    """Storage address and version counter of every tensor: any in-place torch write or a
+    replaced `.data` changes it (kernel writes through the packed arenas do not)."""
+    return tuple((t.data_ptr(), t._version) for t in ts)
+
+
+class OuterParameter(torch.nn.Parameter):
+    """A parameter of a fused device outer model (get_outer_model(..., placement="device")).
+
+    Its mirror defers work the reference does eagerly: compute_pseudo_gradient records the
+    delta instead of computing it, and sync_gradients leaves the packed .grad holding the Σ
+    with the /n pending, so the outer SGD can run all of it in one pass. Reading or assigning
+    `.grad` first completes whatever is pending, so every value a caller observes equals the
+    reference's (src/utils.py:221, src/comm.py:122-123)."""
+
+    def _settle(self) -> None:
+        r = self.__dict__.get("_dl_mirror")
+        m = r() if r is not None else None
+        if m is not None and m.pending:
+            m.settle_grads()
+
+    @property
+    def grad(self):
+        self._settle()
+        return _GRAD.__get__(self)
+
+    @grad.setter
+    def grad(self, value):
+        self._settle()
+        _GRAD.__set__(self, value)
+
+    @grad.deleter
+    def grad(self):
+        self._settle()
+        _GRAD.__delete__(self)
+
+    def __reduce_ex__(self, proto):  # pickles as a plain Parameter (the mirror stays behind)
+        return (torch._utils._rebuild_parameter, (self.data, self.requires_grad, OrderedDict()))
+
+
+def use_outer_parameters(model: torch.nn.Module) -> None:
+    """Replace every parameter of `model` by an OuterParameter over the same data (shared
+    parameters stay shared). Only for a module nothing else references yet: get_outer_model's
+    fresh deep copy."""
+    memo = {}
+    for mod in model.modules():
+        for name, p in list(mod._parameters.items()):
+            if p is None or isinstance(p, OuterParameter):
+                continue
+            q = memo.get(id(p))
+            if q is None:
+                q = memo[id(p)] = OuterParameter(p.data, p.requires_grad)
+            mod._parameters[name] = q
+
+
 class DeviceOuterMirror:
     """Device-resident outer model: the outer parameters, their .grad and
     the optimizer's momentum buffers ARE views into packed HBM arenas, so the reference's
     compute_pseudo_gradient -> sync_gradients -> outer SGD -> sync_inner_model sequence runs
-    as dl_delta_pack -> RCCL all_reduce + dl_unpack_avg -> dl_unpack_sgd -> dl_scatter with no
-    host round trip and no host synchronisation (everything is ordered on the current stream).
-    A host copy is made only when asked for (`.cpu()`, `state_dict()`): torch copies lazily.
+    with no host round trip and no host synchronisation (everything is ordered on the current
+    stream). A host copy is made only when asked for (`.cpu()`, `state_dict()`): torch copies
+    lazily. Chosen by get_outer_model(..., placement="device") or DILOCO_OUTER_PLACEMENT=device.
 
-    Chosen by get_outer_model(..., placement="device") or DILOCO_OUTER_PLACEMENT=device.
-    Tensors replaced by user code (p.data = ..., p.grad = ..., a loaded momentum buffer) are
-    detected by storage address and copied into the arenas before the next use."""
+    fused=False (eager) runs every call as the reference does, one kernel each:
+        dl_delta_pack -> RCCL all_reduce + dl_unpack_avg -> dl_unpack_sgd -> dl_scatter
+        = 12 + (8) + 20 + 8 B per parameter (44 at N > 1, 40 at one peer).
+    fused=True (the default for this placement, DILOCO_OUTER_FUSED=0 turns it off) keeps the
+    observable values and runs the sequence in as few HBM passes as the data flow allows:
+      - compute_pseudo_gradient records the delta (inner params, their signature);
+      - sync_gradients packs each bucket just before its RCCL all_reduce and leaves the /n
+        pending (the packed .grad holds the Σ);
+      - OuterSGD.step runs ONE pass: at one peer dl_delta_pack_sgd (delta, .grad, SGD, θ and
+        the inner params: 28 B/param, the engine's headline kernel); at N > 1 dl_unpack_sgd with
+        the divisor and the inner write (24 B after the 12 B pack);
+      - sync_inner_model verifies that the inner params still hold θ (same tensors, same
+        storage, no version bump on either side since that write) and does nothing; anything
+        else -> dl_scatter as in eager mode.
+    Reading or assigning an outer parameter's .grad completes the pending work first
+    (OuterParameter), so .grad always shows the reference's value. Two consequences differ from
+    the reference and are the price of the fusion: the inner params receive θ_new during
+    OuterSGD.step() rather than in sync_inner_model (train.py reads neither in between), and
+    changing the inner params or θ in place between compute_pseudo_gradient and the call that
+    consumes the delta raises instead of being silently used (writes through `.data` bypass
+    version counters: call invalidate() after them)."""
 
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
-                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS):
+                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = False):
         self.params: List[torch.nn.Parameter] = list(outer_model.parameters())
         if not self.params:
             raise ValueError("outer model has no parameters")
@@ -325,6 +406,10 @@ class DeviceOuterMirror:
                 raise ValueError(f"outer parameter {i} is on {p.device}, expected {self.device}")
             if p.dtype != torch.float32:
                 raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
+        if fused and not all(isinstance(p, OuterParameter) for p in self.params):
+            raise TypeError("fused=True needs OuterParameter parameters (use_outer_parameters): "
+                            "their .grad completes the deferred work")
+        self.fused = fused
         self.numels = [p.numel() for p in self.params]
         self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems)
         self.offs = [int(o) for o in self.tree.seg_off[:-1]]
@@ -338,6 +423,15 @@ class DeviceOuterMirror:
                        "wire": self._make_views(self.d_wire)}
         self._ptrs = {k: [v.data_ptr() for v in vs] for k, vs in self._views.items()}
         self._relay("theta", "data")
+        # fused-mode state
+        self._delta = None   # pending pseudo-gradient: (inner params, their _sig, θ versions)
+        self._div = 1        # pending /n: d_wire holds the Σ of the peers' deltas
+        self._target = None  # (inner params, _sig) of the last compute_pseudo_gradient
+        self._synced = None  # (inner params, _sig, θ versions) when the inner params hold θ
+        if fused:
+            ref = weakref.ref(self)
+            for p in self.params:
+                p.__dict__["_dl_mirror"] = ref
 
     def _make_views(self, arena: torch.Tensor) -> List[torch.Tensor]:
         return [arena[o:o + n].view(p.shape)
@@ -351,18 +445,22 @@ class DeviceOuterMirror:
         exp = self._ptrs[kind]
         if what == "data":
             return all(p.data_ptr() == e for p, e in zip(self.params, exp))
-        return all(p.grad is not None and p.grad.data_ptr() == e
-                   for p, e in zip(self.params, exp))
+        for p, e in zip(self.params, exp):
+            g = _GRAD.__get__(p)
+            if g is None or g.data_ptr() != e:
+                return False
+        return True
 
-    def _relay(self, kind: str, what: str, zero_fill_missing: bool = True) -> None:
-        """Make every parameter's `what` ("data" or "grad") the view of arena `kind`."""
+    def _relay(self, kind: str, what: str, zero_fill_missing: bool = True) -> bool:
+        """Make every parameter's `what` ("data" or "grad") the view of arena `kind`; True if
+        any arena content was replaced."""
         if self._in_place(kind, what):
-            return
+            return False
         views = self._views[kind]
         with torch.no_grad():
             for i, p in enumerate(self.params):
                 v = views[i]
-                cur = p.data if what == "data" else p.grad
+                cur = p.data if what == "data" else _GRAD.__get__(p)
                 if cur is not None and cur.data_ptr() == v.data_ptr():
                     continue
                 if cur is None:
@@ -376,45 +474,114 @@ class DeviceOuterMirror:
                 if what == "data":
                     p.data = v
                 else:
-                    p.grad = v
+                    _GRAD.__set__(p, v)
+        return True
 
-    def invalidate(self) -> None:  # the arenas are the tensors: nothing is cached
-        pass
+    def _relay_theta(self) -> None:
+        if self._relay("theta", "data"):
+            self._synced = None  # θ's arena content changed: the inner params no longer hold it
 
-    def flush(self) -> None:  # nothing is written back: torch copies to the host on demand
-        pass
+    def _theta_versions(self) -> tuple:
+        return tuple(p._version for p in self.params)
+
+    def invalidate(self) -> None:
+        """After writes through `.data` (no version bump): forget that the inner params hold θ."""
+        self._synced = None
+        self._target = None
+
+    # ---- deferred work (fused mode) ------------------------------------------------------
+    @property
+    def pending(self) -> bool:
+        return self._delta is not None or self._div != 1
+
+    def _take_delta(self) -> List[torch.Tensor]:
+        """The pending delta's inner params, checked unchanged since compute_pseudo_gradient
+        and bound to SLOT_INNER."""
+        inner, isig, tver = self._delta
+        self._delta = None
+        if (_sig(inner) != isig or self._theta_versions() != tver
+                or not self._in_place("theta", "data")):
+            raise RuntimeError(
+                "the inner or the outer parameters were modified after compute_pseudo_gradient "
+                "and before the pseudo-gradient was used; the fused device outer model computes "
+                "it when it is first needed (get_outer_model(..., fused=False) or "
+                "DILOCO_OUTER_FUSED=0 computes it eagerly)")
+        self.k.bind(self.tree, SLOT_INNER, inner, self.device)
+        return inner
+
+    def settle_grads(self) -> None:
+        """Complete the pending work so the packed .grad holds the reference's values."""
+        if self._delta is not None:
+            self._take_delta()
+            self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
+        if self._div != 1:
+            div, self._div = self._div, 1
+            self.k.unpack_avg(self.tree, ALL, self.d_wire, div, -1, self.d_wire)
+
+    def flush(self) -> None:
+        """No host copy to write back (torch copies to the host on demand); completes the
+        deferred .grad work."""
+        if self.fused:
+            self.settle_grads()
+
+    def _grad_views(self) -> None:
+        if not self._in_place("wire", "grad"):
+            for p, v, e in zip(self.params, self._views["wire"], self._ptrs["wire"]):
+                g = _GRAD.__get__(p)
+                if g is None or g.data_ptr() != e:
+                    _GRAD.__set__(p, v)
 
     # ---- the four reference operations --------------------------------------------------
     def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
         """outer.grad = outer - inner (src/utils.py:218-221); .grad are views of d_wire."""
-        self._relay("theta", "data")
-        self.k.bind(self.tree, SLOT_INNER, inner_params, self.device)
-        self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
-        if not self._in_place("wire", "grad"):
-            for p, v, e in zip(self.params, self._views["wire"], self._ptrs["wire"]):
-                if p.grad is None or p.grad.data_ptr() != e:
-                    p.grad = v
+        inner = list(inner_params)
+        self._relay_theta()
+        self.k.bind(self.tree, SLOT_INNER, inner, self.device)  # shape errors raise here
+        self._div = 1  # the wire is overwritten: a /n still pending is moot
+        if self.fused:
+            sig = _sig(inner)
+            self._delta = (inner, sig, self._theta_versions())
+            self._target = (inner, sig)
+        else:
+            self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
+        self._grad_views()
 
     def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
         """grad = Σ_peers grad / n (src/comm.py:120-123), in place on the packed .grad."""
-        self._relay("wire", "grad", zero_fill_missing=True)
+        pack = None
+        if self._delta is not None:  # fused: each bucket packed just before its collective
+            self._take_delta()
+            self._relay_theta()
+            self._grad_views()
+
+            def pack(b):
+                self.k.delta_pack(self.tree, b, SLOT_INNER, self.d_theta, self.d_wire)
+        else:
+            if self._div != 1:
+                self.settle_grads()  # a second sync_gradients reduces the averages
+            self._relay("wire", "grad", zero_fill_missing=True)
 
         def view(b):
             lo, hi = self.tree.bucket_ranges[b]
             return self.d_wire[lo:hi]
 
+        div = num_peers if self.fused else 1
         pipelined_buckets(
-            self.tree.n_buckets, lambda b: None,
+            self.tree.n_buckets, pack or (lambda b: None),
             lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
-            lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
+            (lambda b: None) if self.fused else
+            (lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire)),
         )
+        self._div = div
 
     def sgd_step(self, lr: float, momentum: float, nesterov: bool,
                  host_bufs: Optional[List[Optional[torch.Tensor]]]) -> List[Optional[torch.Tensor]]:
         """torch.optim.SGD._single_tensor_sgd over the whole tree; returns the momentum
         buffers (views of d_mom) for the optimizer state."""
-        self._relay("theta", "data")
-        self._relay("wire", "grad", zero_fill_missing=False)
+        delta = self._take_delta() if self._delta is not None else None
+        self._relay_theta()
+        if delta is None:
+            self._relay("wire", "grad", zero_fill_missing=False)
         first = True
         bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
         if momentum != 0:
@@ -432,15 +599,41 @@ class DeviceOuterMirror:
                     for b, v, e in zip(host_bufs, bufs, self._ptrs["mom"]):
                         if b.data_ptr() != e:
                             v.copy_(b)  # e.g. a state_dict loaded into the optimizer
-        self.k.unpack_sgd(self.tree, ALL, self.d_wire, 1, self.d_theta,
-                          self.d_mom if momentum != 0 else None, lr, momentum, nesterov, first, -1)
+        mom = self.d_mom if momentum != 0 else None
+        # the inner params of the last compute_pseudo_gradient take θ_new in the same pass
+        # (fused mode), unless they were modified since
+        target, self._target = self._target, None
+        write = target is not None and (delta is not None or _sig(target[0]) == target[1])
+        if delta is not None:  # one peer: the delta never leaves registers
+            self.k.delta_pack_sgd(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire, mom,
+                                  lr, momentum, nesterov, first)
+        else:
+            if write:
+                self.k.bind(self.tree, SLOT_INNER, target[0], self.device)
+            # a pending /n stays pending: the wire keeps the Σ, .grad settles it when read
+            self.k.unpack_sgd(self.tree, ALL, self.d_wire, self._div, self.d_theta, mom, lr,
+                              momentum, nesterov, first, SLOT_INNER if write else -1)
+        self._synced = ((target[0], target[1], self._theta_versions()) if write else None)
         return bufs
 
     def copy_to_inner(self, inner_params: Sequence[torch.Tensor]) -> None:
-        """inner = outer (src/utils.py:223-226), scattered from HBM."""
-        self._relay("theta", "data")
-        self.k.bind(self.tree, SLOT_INNER, inner_params, self.device)
+        """inner = outer (src/utils.py:223-226): verified no-op after a fused step that
+        already wrote these inner params, else scattered from HBM."""
+        inner = list(inner_params)
+        self._target = None
+        if self._delta is not None:  # the inner params are about to change: use them first
+            self._take_delta()
+            self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
+        self._relay_theta()
+        s = self._synced
+        if (s is not None and len(s[0]) == len(inner)
+                and all(a is b for a, b in zip(s[0], inner))
+                and _sig(inner) == s[1] and self._theta_versions() == s[2]):
+            return
+        self.k.bind(self.tree, SLOT_INNER, inner, self.device)
         self.k.scatter(self.tree, ALL, self.d_theta, SLOT_INNER)
+        if self.fused:
+            self._synced = (inner, _sig(inner), self._theta_versions())
 
     def close(self) -> None:
         self.tree.close()

@@ -113,10 +113,6 @@ class PackedTree:
         """Launch shape of the walker kernels (speed only; results are identical)."""
         _lib.call("dl_tree_tune", self.handle, int(max_blocks), int(flags))
 
-    def slot(self, period_ticks: int = 0, read_ticks: int = 0) -> None:
-        """Clock-slotted launches of the SGD / delta walkers (dl_tree_slot; speed only)."""
-        _lib.call("dl_tree_slot", self.handle, int(period_ticks), int(read_ticks))
-
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:
             try:

@@ -9,8 +9,11 @@ promotion of the fp32 metadata plane with the payload: fp32/bf16/fp16 -> fp32, f
 
 Dispatch is on the payload's device, as the reference frames on `tensor.device`
 (src/serializer.py:12):
-  GPU  one HIP kernel (dl_serialize: 2 metadata writes + a converting copy) instead of
-       torch.empty + two indexed writes + reshape + cat; fp32/bf16/fp16 payloads. Without
+  GPU  one HIP kernel (dl_serialize: 2 metadata writes + a converting copy; dl_serialize_f64
+       for fp64 payloads, whose frame is fp64 as torch.cat makes it) instead of torch.empty +
+       two indexed writes + reshape + cat. The frame keeps the payload's autograd graph, as
+       torch.cat's does: a payload that requires grad is framed through an autograd.Function
+       whose backward hands plane 1's gradient back in the payload's dtype. Without
        libdiloco_hip.so this raises (no fallback for device tensors).
   CPU  the same frame built with torch ops in host memory (the reference's --device cpu runs,
        tests/test_memorize.py:35-39).
@@ -28,6 +31,35 @@ Metadata = Tuple[int, int]  # (root, local_micro_step)
 _SRC = {torch.float32: _lib.DL_F32, torch.bfloat16: _lib.DL_BF16, torch.float16: _lib.DL_F16}
 
 
+def _frame_device(tensor: torch.Tensor, m0: float, m1: float) -> torch.Tensor:
+    """dl_serialize(_f64) of a device payload into a new (2, *shape) frame."""
+    src = tensor.detach().contiguous()
+    s = torch.cuda.current_stream(tensor.device).cuda_stream
+    if tensor.dtype == torch.float64:
+        out = torch.empty((2, *tensor.shape), dtype=torch.float64, device=tensor.device)
+        _lib.call("dl_serialize_f64", src.data_ptr(), src.numel(), m0, m1, out.data_ptr(), s)
+        return out
+    if tensor.dtype not in _SRC:
+        raise TypeError(f"serialize: payload dtype {tensor.dtype} (fp32/bf16/fp16/fp64)")
+    out = torch.empty((2, *tensor.shape), dtype=torch.float32, device=tensor.device)
+    _lib.call("dl_serialize", src.data_ptr(), _SRC[tensor.dtype], src.numel(), m0, m1,
+              out.data_ptr(), s)
+    return out
+
+
+class _Frame(torch.autograd.Function):
+    """The HIP frame with torch.cat's backward: d(frame)/d(payload) is plane 1, cast back."""
+
+    @staticmethod
+    def forward(ctx, tensor, m0, m1):
+        ctx.dtype = tensor.dtype
+        return _frame_device(tensor, m0, m1)
+
+    @staticmethod
+    def backward(ctx, grad):
+        return grad[1].to(ctx.dtype), None, None
+
+
 class Serializer:
     def __init__(self, shape: Tuple[int, ...]):
         self.shape = (2, *shape)
@@ -38,14 +70,10 @@ class Serializer:
             raise IndexError(f"index {n} is out of bounds for dimension 0 with size {n}")
         if tensor.device.type != "cuda":
             return self._frame_host(tensor, metadata)
-        if tensor.dtype not in _SRC:
-            raise TypeError(f"serialize: payload dtype {tensor.dtype} (fp32/bf16/fp16)")
-        src = tensor.detach().contiguous()
-        out = torch.empty((2, *tensor.shape), dtype=torch.float32, device=tensor.device)
-        _lib.call("dl_serialize", src.data_ptr(), _SRC[tensor.dtype], n, float(metadata[0]),
-                  float(metadata[1]), out.data_ptr(),
-                  torch.cuda.current_stream(tensor.device).cuda_stream)
-        return out
+        m0, m1 = float(metadata[0]), float(metadata[1])
+        if tensor.requires_grad and torch.is_grad_enabled():
+            return _Frame.apply(tensor, m0, m1)
+        return _frame_device(tensor, m0, m1)
 
     @staticmethod
     def _frame_host(tensor: torch.Tensor, metadata: Metadata) -> torch.Tensor:

@@ -23,6 +23,11 @@ DILOCO_OUTER_PLACEMENT environment variable, "host" if unset):
             .grad and momentum buffers are views of packed HBM arenas
             (mirror.DeviceOuterMirror); no PCIe traffic and no host synchronisation per outer
             step. Host copies are made lazily by torch (`.cpu()`, `state_dict()`).
+            fused (`get_outer_model(..., fused=)`, default from DILOCO_OUTER_FUSED, on if
+            unset): the four calls run as one HBM pass at one peer (dl_delta_pack_sgd, the
+            engine's kernel) and pack -> RCCL -> one SGD pass at N > 1; the parameters are
+            mirror.OuterParameter, whose .grad completes the deferred work when read, and
+            sync_inner_model is a verified no-op after the step (see DeviceOuterMirror).
 
 Write-back of the host placement (`get_outer_model(..., write_back=)`, default from
 DILOCO_HOST_WRITEBACK, "sync" if unset): "sync" -- every call returns with the host tensors
@@ -42,13 +47,14 @@ import torch.nn as nn
 from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
-from .mirror import WRITE_BACKS, DeviceOuterMirror, HostOuterMirror
+from .mirror import WRITE_BACKS, DeviceOuterMirror, HostOuterMirror, use_outer_parameters
 from .optim import OuterSGD
 
 _ATTR = "_diloco_mirror"
 _OUTER = "_diloco_outer"
 _PLACEMENT = "_diloco_placement"
 _WRITE_BACK = "_diloco_write_back"
+_FUSED = "_diloco_fused"
 PLACEMENTS = ("host", "device")
 
 
@@ -73,7 +79,8 @@ def outer_mirror(outer_model: nn.Module, device=None):
             p = next(outer_model.parameters(), None)
             if p is None:
                 raise ValueError("outer model has no parameters")
-            m = DeviceOuterMirror(outer_model, p.device, kernels=k)
+            m = DeviceOuterMirror(outer_model, p.device, kernels=k,
+                                  fused=getattr(outer_model, _FUSED, False))
             object.__setattr__(outer_model, _ATTR, m)
             return m
         if device is None:
@@ -96,11 +103,12 @@ def _inner_device(inner_model: nn.Module) -> torch.device:
 
 
 def get_outer_model(inner_model: nn.Module, placement: str = None,
-                    write_back: str = None) -> nn.Module:
+                    write_back: str = None, fused: bool = None) -> nn.Module:
     """Initializes the outer model from the inner model (src/utils.py:213-216).
 
     placement "host" (the reference's, default) or "device"; write_back "sync" (default) or
-    "deferred" for the host placement (see the module docstring)."""
+    "deferred" for the host placement; fused (default on) for the device placement (see the
+    module docstring)."""
     if placement is None:
         placement = os.environ.get("DILOCO_OUTER_PLACEMENT", "host")
     if placement not in PLACEMENTS:
@@ -109,6 +117,8 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
         write_back = os.environ.get("DILOCO_HOST_WRITEBACK", "sync")
     if write_back not in WRITE_BACKS:
         raise ValueError(f"write_back {write_back!r}: one of {WRITE_BACKS}")
+    if fused is None:
+        fused = os.environ.get("DILOCO_OUTER_FUSED", "1") not in ("0", "")
     outer_model = copy.deepcopy(inner_model)
     if placement == "host":
         outer_model = outer_model.to("cpu")
@@ -125,7 +135,10 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     object.__setattr__(outer_model, _OUTER, True)  # get_optimizer: SGD here is the outer SGD
     object.__setattr__(outer_model, _PLACEMENT, placement)
     object.__setattr__(outer_model, _WRITE_BACK, write_back)
+    object.__setattr__(outer_model, _FUSED, bool(fused) and placement == "device")
     if placement == "device":
+        if fused:
+            use_outer_parameters(outer_model)
         outer_mirror(outer_model)  # lay the parameters out in the packed HBM arena now
     elif write_back == "deferred":
         # a checkpoint of the outer model waits for the write-back in flight

@@ -30,7 +30,7 @@ extern "C" {
 
 #define DL_API __attribute__((visibility("default")))
 
-#define DL_ABI_VERSION 1
+#define DL_ABI_VERSION 2
 #define DL_ALIGN_ELEMS 64      /* segment start alignment in the packed space: 256 B of fp32 */
 #define DL_CHUNK_ELEMS 4096    /* work unit of every segment walker: 16 KiB of fp32 */
 #define DL_ALL_BUCKETS (-1)
@@ -96,32 +96,27 @@ DL_API int dl_tree_bucket_chunks(dl_tree_t tree, int32_t bucket, int32_t* chunk_
  * pinned slots and expanded into the slot's per-chunk table by a kernel, so rebinding grads
  * that torch reallocated (zero_grad(set_to_none=True) before every inner step,
  * src/train.py:164) costs no host synchronisation. Kernels queued on `stream` before the
- * call still see the previous table; kernels on other streams must be ordered by the caller. */
+ * call still see the previous table. A bind or kernel that uses a slot on another stream than
+ * the slot's previous bind or kernel first waits for that one (an event per slot), so a
+ * table is never rewritten under, or read before, work the caller did not order. */
 DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, int32_t n,
                         dl_stream_t stream);
 /* Launch shape of every walker kernel on this tree: max_blocks caps the grid (0 = one
- * workgroup per chunk, the default); flags = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES |
- * DL_TUNE_WT_STORES | DL_TUNE_REVERSE selects non-temporal loads / non-temporal stores /
- * write-through stores (sc1; wins over NT_STORES; the int8 encoder's payload stays NT) / a
- * last-to-first chunk order for every kernel, DL_TUNE_AUTO (the default) the measured
- * per-kernel choice (NT loads everywhere; NT stores in the SGD kernels and, over launches of
+ * workgroup per chunk, the default); flags = DL_TUNE_AUTO (the default: the measured
+ * per-kernel choice -- NT loads everywhere; NT stores in the SGD kernels and, over launches of
  * more than 2^28 elements, in dl_delta_pack / dl_gather / dl_scatter / dl_unpack_avg;
- * write-through stores in dl_unpack_sgd_q8 below that size). Results are identical for
- * every setting; only speed differs. */
+ * write-through stores in dl_unpack_sgd_q8 below that size) or DL_TUNE_NT_LOADS [|
+ * DL_TUNE_NT_STORES] for every kernel. Plain loads and DL_TUNE_WT_STORES (write-through, sc1)
+ * for every kernel exist only in the tuning build (make TUNING=1, dl_tuning_build() == 1);
+ * the product library rejects them with DL_E_ARG. Results are identical for every setting;
+ * only speed differs. */
 #define DL_TUNE_NT_LOADS 1
 #define DL_TUNE_NT_STORES 2
-#define DL_TUNE_REVERSE 4 /* walk chunks last to first */
-#define DL_TUNE_WT_STORES 8 /* write-through (sc1) stores */
+#define DL_TUNE_WT_STORES 8 /* write-through (sc1) stores; tuning build only */
 #define DL_TUNE_AUTO (-1)
 DL_API int dl_tree_tune(dl_tree_t tree, int32_t max_blocks, int32_t flags);
-
-/* Clock-slotted launches of the tree's SGD and delta kernels (dl_delta_pack_sgd,
- * dl_delta_sgd, dl_unpack_sgd, dl_delta_pack): a grid of as many workgroups as fit on the GPU
- * at once, whose rounds (one chunk per workgroup) start every period_ticks ticks of the GPU's
- * 100 MHz real-time counter, the stores of a round read_ticks after its loads -- the chip reads,
- * then writes, instead of a steady mix. period_ticks = 0 (the default) turns it
- * off. Results are identical either way; only the timing changes. */
-DL_API int dl_tree_slot(dl_tree_t tree, int32_t period_ticks, int32_t read_ticks);
+/* 1 in the tuning build (every load / store policy instantiated), 0 in the product library. */
+DL_API int dl_tuning_build(void);
 
 /* ---- hot-path kernels ----------------------------------------------------------------- */
 
@@ -241,6 +236,12 @@ DL_API int dl_unpack_sgd_q8(dl_tree_t tree, int32_t bucket, const void* slots,
  * the reference leaves it uninitialised (torch.empty, src/serializer.py:12). numel >= 2. */
 DL_API int dl_serialize(const void* src, int32_t src_dtype, int64_t numel, float meta0,
                         float meta1, float* out, dl_stream_t stream);
+/* The fp64 frame (torch.cat promotes the fp32 metadata plane to the fp64 payload's dtype):
+ * out is fp64 of 2*numel elements, out[0] = (double)meta0, out[1] = (double)meta1 (the
+ * metadata rounds through fp32 first, as the reference's fp32 metadata tensor does),
+ * out[numel + i] = src[i]. */
+DL_API int dl_serialize_f64(const double* src, int64_t numel, float meta0, float meta1,
+                            double* out, dl_stream_t stream);
 
 /* ---- synthetic parameter trees (bench / tests) ------------------------------------------
  * dst[i] = base + u(seed, stream_id, i) * scale (+ add[i] if add != NULL), with

@@ -33,13 +33,19 @@ def test_library_exports_every_declared_symbol():
     assert lib.dl_abi_version() == _lib.ABI_VERSION
 
 
+def test_product_library_is_not_the_tuning_build():
+    """The shipped libdiloco_hip.so instantiates the AUTO policies only."""
+    assert _lib.load().dl_tuning_build() == 0
+
+
 def test_header_constants_match_python_mirror():
     src = open(HEADER).read()
     consts = dict(re.findall(r"#define (DL_\w+) \(?(-?\d+)\)?", src))
     assert int(consts["DL_TUNE_AUTO"]) == _lib.TUNE_AUTO
     assert (int(consts["DL_TUNE_NT_LOADS"]), int(consts["DL_TUNE_NT_STORES"]),
-            int(consts["DL_TUNE_REVERSE"]), int(consts["DL_TUNE_WT_STORES"])) == (
-        _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_REVERSE, _lib.TUNE_WT_STORES)
+            int(consts["DL_TUNE_WT_STORES"])) == (
+        _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_WT_STORES)
+    assert "DL_TUNE_REVERSE" not in consts and "dl_tree_slot" not in src
     assert (int(consts["DL_COPY_WIDE"]), int(consts["DL_COPY_READ"]),
             int(consts["DL_COPY_WRITE"])) == (_lib.COPY_WIDE, _lib.COPY_READ, _lib.COPY_WRITE)
     assert int(consts["DL_ALIGN_ELEMS"]) == _lib.ALIGN_ELEMS

@@ -1,4 +1,4 @@
-"""BASELINE configs #4 and #5 at their full 1.3B workload (T1.3B: 292 tensors, 1,313,722,368
+"""BASELINE config #3 at its full T125 size, and configs #4 and #5 at their full 1.3B workload (T1.3B: 292 tensors, 1,313,722,368
 params, 25 buckets of <= 256 MiB), several replicas on the one GPU of the box.
 
 The collectives are emulated bucket by bucket with torch on the device, in rank order (what
@@ -44,9 +44,9 @@ def _free_hbm():
     torch.cuda.empty_cache()
 
 
-def _picks(full_wte):
+def _picks(full_wte, spec=SPEC):
     """(tensor, first element, count): wte, the first block's tensors, the last tensor."""
-    numels = SPEC.numels()
+    numels = spec.numels()
     wte = (0, 0, numels[0]) if full_wte else (0, 37_000_011, 4 << 20)
     return [wte] + [(t, 0, numels[t]) for t in range(1, 10)] + [(len(numels) - 1, 0, numels[-1])]
 
@@ -62,11 +62,11 @@ def _slice_inputs(t, lo, m, step, ranks, theta):
     return out
 
 
-def _expected(n, wire, full_wte):
+def _expected(n, wire, full_wte, spec=SPEC):
     """Oracle θ and momentum on the sampled slices after each of STEPS outer steps."""
-    init = SPEC.init_spec()
+    init = spec.init_spec()
     exp = {}
-    for t, lo, m in _picks(full_wte):
+    for t, lo, m in _picks(full_wte, spec):
         b, sc = init[t]
         th = (F32(b) + synth.uniform(synth.OUTER_SEED, t, m, start=lo) * F32(sc)).astype(F32)
         th32 = th.copy()
@@ -100,15 +100,16 @@ def _expected(n, wire, full_wte):
     return exp
 
 
-def _replicas(n, wire=torch.float32, shard=False, exchange="rccl"):
-    shapes = [s for _, s in SPEC.params()]
+def _replicas(n, wire=torch.float32, shard=False, exchange="rccl", spec=SPEC, buckets=25):
+    shapes = [s for _, s in spec.params()]
     engines, inners = [], []
     for r in range(n):
-        inner = [t.view(s) for t, s in zip(synth.outer_tree_device(SPEC, DEV), shapes)]
+        inner = [t.view(s) for t, s in zip(synth.outer_tree_device(spec, DEV), shapes)]
         engines.append(OuterSync(inner, world_size=n, wire_dtype=wire, shard=shard, rank=r,
                                  exchange=exchange))
         inners.append(inner)
-    assert engines[0].tree.n_buckets == 25
+    if buckets is not None:
+        assert engines[0].tree.n_buckets == buckets
     return engines, inners
 
 
@@ -186,7 +187,7 @@ def _a2a_step(engines, inners, step):
     torch.cuda.synchronize()
 
 
-def _check(engines, inners, exp, step, n, full_wte, wire, sharded=False):
+def _check(engines, inners, exp, step, n, full_wte, wire, sharded=False, spec=SPEC):
     e0 = engines[0]
     mom_full = e0.momentum_full() if not sharded else None
     if sharded:  # assemble the momentum shards of every replica (the all-gather of the state)
@@ -194,7 +195,7 @@ def _check(engines, inners, exp, step, n, full_wte, wire, sharded=False):
         for b, (lo, hi) in enumerate(e0.tree.bucket_ranges):
             mom_full[lo:hi] = torch.cat([e._shard(e.mom_shard, b) for e in engines])
     worst = 0.0
-    for t, lo, m in _picks(full_wte):
+    for t, lo, m in _picks(full_wte, spec):
         th_exp, buf_exp, th32 = exp[(t, lo, step)]
         o = int(e0.tree.seg_off[t]) + lo
         for e, inner in zip(engines, inners):
@@ -207,7 +208,7 @@ def _check(engines, inners, exp, step, n, full_wte, wire, sharded=False):
             if th0 is not None:
                 u_bf, u_32 = th0 - th_exp, exp[(t, lo, step - 1)][2] - th32
             else:
-                init = SPEC.init_spec()[t]
+                init = spec.init_spec()[t]
                 base = (F32(init[0]) + synth.uniform(synth.OUTER_SEED, t, m, start=lo)
                         * F32(init[1])).astype(F32)
                 u_bf, u_32 = base - th_exp, base - th32
@@ -272,5 +273,28 @@ def test_t13b_eight_replicas_bf16_wire_ordered_exchange():
     for s in range(1, STEPS + 1):
         _a2a_step(engines, inners, s)
         _check(engines, inners, exp, s, 8, False, "bf16_a2a", sharded=True)
+    for e in engines:
+        e.close()
+
+
+T125 = get_tree("t125")
+
+
+@pytest.mark.parametrize("path", ["replicated", "sharded"])
+def test_t125_two_replicas_config3_vs_oracle(path):
+    """BASELINE config #3 (T125: 148 tensors, 124,475,904 params, DP = 2, fp32) at full size
+    against the C oracle (src/comm.py:122-123, src/utils.py:221): 2 emulated replicas, 2 outer
+    steps, through the replicated path (delta_pack -> Σ -> unpack_sgd with the inner write)
+    and the sharded one (reduce-scatter -> dl_shard_sgd -> all-gather -> dl_scatter). θ, the
+    momentum and the inner params bit-exact on wte (38.6 M elements, whole), the first block
+    and the last tensor; every replica's whole θ identical."""
+    exp = _expected(2, "f32", full_wte=True, spec=T125)
+    engines, inners = _replicas(2, shard=path == "sharded", spec=T125, buckets=None)
+    assert engines[0].tree.n_buckets >= 2  # 256 MiB buckets: the bucketed exchange
+    assert engines[0].sharded == (path == "sharded")
+    step = _sharded_step if path == "sharded" else _replicated_step
+    for s in range(1, STEPS + 1):
+        step(engines, inners, s)
+        _check(engines, inners, exp, s, 2, True, "f32", sharded=path == "sharded", spec=T125)
     for e in engines:
         e.close()

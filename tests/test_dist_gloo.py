@@ -71,13 +71,19 @@ def _worker(rank, world, port, mode, num_stages, out):
     shapes = [s for _, s in spec.params()]
     theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
     rec = {}
-    if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_host"):
+    if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_host",
+                "dropin_device_quiet", "dropin_device_eager"):
         from diloco_amd.utils import flush_outer_model, has_mirror
 
         deferred = mode == "dropin_deferred"
+        # quiet: nothing reads the outer model between the four calls (src/train.py:261-269),
+        # so the fused device model defers the delta and the /n into its one SGD pass
+        quiet = mode == "dropin_device_quiet"
+        device = mode.startswith("dropin_device")
         inner = _micro_module(theta0, shapes)
-        outer = get_outer_model(inner, placement="device" if mode == "dropin_device" else None,
-                                write_back="deferred" if deferred else None)
+        outer = get_outer_model(inner, placement="device" if device else None,
+                                write_back="deferred" if deferred else None,
+                                fused=mode != "dropin_device_eager")
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
         assert type(opt).__name__ == "OuterSGD"
         from diloco_amd.utils import outer_mirror
@@ -85,7 +91,9 @@ def _worker(rank, world, port, mode, num_stages, out):
             assert not has_mirror(outer)
         else:
             assert type(outer_mirror(outer)).__name__ == (
-                "DeviceOuterMirror" if mode == "dropin_device" else "HostOuterMirror")
+                "DeviceOuterMirror" if device else "HostOuterMirror")
+            if device:
+                assert outer_mirror(outer).fused == (mode != "dropin_device_eager")
         comm = TrainingComm(world_, (1, 1, 32), None)
         for s in range(1, MICRO_STEPS + 1):
             prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
@@ -98,7 +106,7 @@ def _worker(rank, world, port, mode, num_stages, out):
 
             # deferred write-back: outer step 1 flushes after every call (the mid-sequence
             # flush path), outer step 2 reads the host tensors only after sync_inner_model
-            mid = not deferred or s == 1
+            mid = not quiet and (not deferred or s == 1)
             compute_pseudo_gradient(inner, outer)
             if deferred and s == 1:
                 flush_outer_model(outer)
@@ -109,7 +117,7 @@ def _worker(rank, world, port, mode, num_stages, out):
                 flush_outer_model(outer)
             if mid:
                 rec[f"avg_s{s}"] = host(p.grad for p in outer.parameters())
-            elif len(world_.dp_ranks) > 1:  # still the previous step's averages on the host
+            elif deferred and len(world_.dp_ranks) > 1:  # the host still has step 1's averages
                 assert host(p.grad for p in outer.parameters()).tobytes() == rec["avg_s1"].tobytes()
             opt.step()
             if deferred and s == 1:
@@ -119,7 +127,8 @@ def _worker(rank, world, port, mode, num_stages, out):
                 rec[f"buf_s{s}"] = host(opt.state[p]["momentum_buffer"] for p in outer.parameters())
             sync_inner_model(outer, inner)
             if not mid:
-                flush_outer_model(outer)
+                if deferred:  # quiet: reading .grad itself completes the pending /n
+                    flush_outer_model(outer)
                 rec[f"avg_s{s}"] = host(p.grad for p in outer.parameters())
                 rec[f"theta_s{s}"] = host(outer.parameters())
                 rec[f"buf_s{s}"] = host(opt.state[p]["momentum_buffer"] for p in outer.parameters())
@@ -273,7 +282,8 @@ def _run(mode, world, num_stages=1):
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_deferred", "engine",
+@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_device_quiet",
+                                  "dropin_device_eager", "dropin_deferred", "engine",
                                   "engine_ar", "engine_a2a", "dropin_host"])
 def test_two_peers_match_reference_bit_exact(mode):
     g = load_npz("micro_n2.npz")
@@ -285,13 +295,14 @@ def test_two_peers_match_reference_bit_exact(mode):
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
             if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
-    if mode.startswith("dropin"):
+    if mode.startswith("dropin") and mode != "dropin_device_quiet":
         assert recs[0]["delta_s1"].tobytes() == g["delta_s1_r0"].tobytes()
         assert recs[1]["delta_s1"].tobytes() == g["delta_s1_rlast"].tobytes()
 
 
 @pytest.mark.parametrize("mode,world", [("dropin", 4), ("engine", 4), ("engine_ar", 4),
-                                        ("dropin", 8), ("engine", 8), ("dropin_host", 4)])
+                                        ("dropin", 8), ("engine", 8), ("dropin_host", 4),
+                                        ("dropin_device_quiet", 4)])
 def test_four_and_eight_peers_match_reference_normwise(mode, world):
     """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""
     from diloco_amd.trees import get_tree

@@ -50,9 +50,11 @@ def _flat(ts):
 
 
 def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=None,
-                 write_back=None):
+                 write_back=None, quiet=False, fused=None):
     """The reference's outer step sequence with the drop-in functions (this process = DP
-    rank `rank` of `n`; the default process group must exist)."""
+    rank `rank` of `n`; the default process group must exist). quiet: nothing is read between
+    the four calls (src/train.py:261-269 reads nothing), so a fused device outer model defers
+    the delta and the /n into its one SGD pass; the values are read after sync_inner_model."""
     from diloco_amd import synth
     from diloco_amd.comm import TrainingComm
     from diloco_amd.trees import get_tree
@@ -64,7 +66,7 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
     shapes = [s for _, s in spec.params()]
     inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cpu")
     # src/train.py:382: before the inner model moves
-    outer = get_outer_model(inner, placement, write_back=write_back)
+    outer = get_outer_model(inner, placement, write_back=write_back, fused=fused)
     deferred = write_back == "deferred"
     inner = inner.to("cuda:0")
     if placement == "device":
@@ -84,7 +86,7 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
                 p.copy_(torch.from_numpy(v).view(p.shape))
         # deferred write-back: outer step 1 flushes after every call, step 2 reads the host
         # tensors only after sync_inner_model's write-back (waited for by the flush)
-        mid = not deferred or s == 1
+        mid = not quiet and (not deferred or s == 1)
         compute_pseudo_gradient(inner, outer)
         if deferred and mid:
             flush_outer_model(outer)
@@ -103,7 +105,8 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
             rec[f"buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"] for p in outer.parameters())
         sync_inner_model(outer, inner)
         if not mid:
-            flush_outer_model(outer)
+            if deferred:  # quiet: reading .grad completes the fused model's pending work
+                flush_outer_model(outer)
             rec[f"delta_s{s}"] = rec[f"avg_s{s}"] = _flat(p.grad for p in outer.parameters())
             rec[f"theta_s{s}"] = _flat(outer.parameters())
             rec[f"buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"] for p in outer.parameters())
@@ -123,17 +126,20 @@ def _init_single():
         dist.init_process_group("gloo", init_method=f"file://{f}", rank=0, world_size=1)
 
 
-@pytest.mark.parametrize("stock_sgd,placement,write_back", [
-    (False, "host", "sync"), (True, "host", "sync"), (False, "device", "sync"),
-    (False, "host", "deferred")])
-def test_dropin_single_peer_matches_reference(stock_sgd, placement, write_back):
+@pytest.mark.parametrize("stock_sgd,placement,write_back,quiet,fused", [
+    (False, "host", "sync", False, None), (True, "host", "sync", False, None),
+    (False, "device", "sync", False, True), (False, "device", "sync", True, True),
+    (False, "device", "sync", False, False), (True, "device", "sync", True, True),
+    (False, "host", "deferred", False, None)])
+def test_dropin_single_peer_matches_reference(stock_sgd, placement, write_back, quiet, fused):
     """The reference's call sequence, outer model on the host (its placement) or in HBM
     (placement="device"); torch's own CPU SGD on the host outer model as
     well (the mirror must see its in-place updates); the host placement with the deferred
     write-back (side-stream DMAs issued by sync_inner_model)."""
     _init_single()
     g = load_npz("micro_n1.npz")
-    rec = _outer_steps(0, 1, stock_sgd=stock_sgd, placement=placement, write_back=write_back)
+    rec = _outer_steps(0, 1, stock_sgd=stock_sgd, placement=placement, write_back=write_back,
+                       quiet=quiet, fused=fused)
     for s in (1, 2):
         assert rec[f"delta_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()
         assert rec[f"avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()  # n=1: no sync
@@ -188,9 +194,11 @@ def _worker(rank, world, port, mode, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     rec = {}
-    if mode in ("dropin", "dropin_device", "dropin_deferred"):
-        rec = _outer_steps(rank, world, placement="device" if mode == "dropin_device" else None,
-                           write_back="deferred" if mode == "dropin_deferred" else None)
+    if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_device_quiet"):
+        rec = _outer_steps(rank, world,
+                           placement="device" if mode.startswith("dropin_device") else None,
+                           write_back="deferred" if mode == "dropin_deferred" else None,
+                           quiet=mode == "dropin_device_quiet")
     elif mode in ("engine", "engine_ar"):
         from diloco_amd import synth
         from diloco_amd.outer import OuterSync
@@ -301,8 +309,8 @@ def _run(mode, world=2):  # noqa: D401
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_deferred", "engine",
-                                  "engine_ar"])
+@pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_device_quiet",
+                                  "dropin_deferred", "engine", "engine_ar"])
 def test_two_peers_on_gpu_match_reference(mode):
     g = load_npz("micro_n2.npz")
     for rec in _run(mode):
@@ -382,6 +390,31 @@ def test_serializer_matches_reference_fixture():
         assert torch.equal(t, y[1])
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+def test_serializer_device_frame_keeps_autograd_and_promotes_like_cat(dtype):
+    """src/serializer.py:15 is torch.cat([meta_plane, tensor]): the frame's dtype is the
+    promotion of fp32 with the payload's (fp64 stays fp64) and it keeps the payload's graph.
+    The HIP frame equals the host restatement of that cat bit for bit and backpropagates
+    plane 1's gradient to the payload in its own dtype."""
+    from diloco_amd.serializer import Serializer
+
+    g = torch.Generator().manual_seed(11)
+    x0 = torch.randn(3, 5, 7, generator=g, dtype=torch.float64).to(dtype)
+    x = x0.clone().cuda().requires_grad_(True)
+    s = Serializer((3, 5, 7))
+    y = s.serialize(x, (3, 1 << 20))
+    ref = Serializer._frame_host(x0, (3, 1 << 20))  # torch.stack/cat on the host
+    assert y.is_cuda and y.dtype == ref.dtype == torch.promote_types(torch.float32, dtype)
+    assert y.requires_grad and y.grad_fn is not None
+    assert torch.equal(y[1].detach().cpu(), ref[1])
+    assert y[0].flatten()[:2].tolist() == [3.0, float(1 << 20)]
+    w = torch.randn(3, 5, 7, generator=g, dtype=torch.float64).to(y.dtype).cuda()
+    (y[1] * w).sum().backward()
+    assert x.grad.dtype == dtype and torch.equal(x.grad.cpu(), w.to(dtype).cpu())
+    with torch.no_grad():
+        assert s.serialize(x, (0, 1)).grad_fn is None
+
+
 def test_serializer_errors_and_large_payload():
     from diloco_amd.serializer import Serializer
 
@@ -396,3 +429,48 @@ def test_serializer_errors_and_large_payload():
     xb = torch.randn(3, 1001, device="cuda").to(torch.bfloat16)
     yb = Serializer((3, 1001)).serialize(xb, (1, 2))
     assert torch.equal(yb[1], xb.float())
+
+
+def test_t125_fused_device_dropin_bit_exact_vs_oracle():
+    """The reference's four calls at full T125 size (148 tensors, 124,475,904 params) on the
+    fused device outer model, nothing read in between: each outer step is one
+    dl_delta_pack_sgd and sync_inner_model a verified no-op. θ, momentum, .grad and the inner
+    params bit-exact vs the C oracle on every tensor after each of 2 outer steps."""
+    from diloco_amd import synth
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+    from oracle import oracle
+
+    _init_single()
+    spec = get_tree("t125")
+    shapes = [s for _, s in spec.params()]
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList(
+        [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"),
+                                                       shapes)])
+    outer = get_outer_model(inner, "device")
+    assert outer._diloco_mirror.fused
+    opt = get_optimizer(outer, SGD_CFG)
+    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    st = oracle.OuterState([p.detach().cpu().numpy().reshape(-1) for p in outer.parameters()])
+    for s in (1, 2):
+        synth.inner_tree_device([p.detach().view(-1) for p in outer.parameters()], s, 0,
+                                out=[p.data.view(-1) for p in inner.parameters()])
+        compute_pseudo_gradient(inner, outer)
+        comm.sync_gradients(outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        inner_host = [synth.values(synth.noise_seed(s, 0), t, x.size, 0.0, synth.NOISE_SCALE, add=x)
+                      for t, x in enumerate(st.theta)]
+        delta = st.step([inner_host])[0][0]
+        for t, (p, q) in enumerate(zip(outer.parameters(), inner.parameters())):
+            th = p.detach().cpu().numpy().reshape(-1)
+            assert th.tobytes() == st.theta[t].tobytes(), (s, t)
+            assert q.detach().cpu().numpy().reshape(-1).tobytes() == st.theta[t].tobytes()
+            buf = opt.state[p]["momentum_buffer"].cpu().numpy().reshape(-1)
+            assert buf.tobytes() == st.buf[t].tobytes(), (s, t)
+            assert p.grad.cpu().numpy().reshape(-1).tobytes() == delta[t].tobytes(), (s, t)

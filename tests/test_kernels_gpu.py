@@ -340,64 +340,15 @@ def test_delta_pack_sgd_equals_two_kernel_pair(wire, momentum, nesterov, misalig
             assert p.cpu().numpy().tobytes() == q.cpu().numpy().tobytes()
 
 
-@pytest.mark.parametrize("kernel", ["delta_pack_sgd", "delta_sgd", "two_kernel"])
-@pytest.mark.parametrize("period,read", [(2, 1), (3000, 1140), (20000, 7600)])
-@pytest.mark.parametrize("misaligned", [False, True])
-def test_slotted_launches_are_bit_identical(kernel, period, read, misaligned):
-    """dl_tree_slot (a resident grid whose rounds follow the GPU's real-time counter) changes
-    only the timing: θ, momentum, the wire and the inner params equal the plain walker's bit
-    for bit -- with more chunks than resident workgroups (several rounds each), ragged tails,
-    the scalar path, a period so short that every round is late and one far longer than a
-    round."""
-    sizes = RAGGED + [2500 * 4096 + 77]
-    g0 = torch.Generator().manual_seed(31)
-    host = [torch.randn(n, generator=g0) for n in sizes]
-
-    def place():
-        if not misaligned:
-            return [h.to(DEV) for h in host]
-        base = torch.empty(sum(sizes) + len(sizes), device=DEV)
-        out, o = [], 1
-        for h in host:
-            out.append(base[o:o + h.numel()])
-            out[-1].copy_(h)
-            o += h.numel() + 1
-        return out
-
-    kw = {"delta_pack_sgd": dict(fuse_single=True, keep_wire=True),
-          "delta_sgd": dict(fuse_single=True),
-          "two_kernel": dict(fuse_single=False, tile_chunks=0)}[kernel]
-    pa, pb = place(), place()
-    ea = OuterSync(pa, world_size=1, **kw)
-    eb = OuterSync(pb, world_size=1, **kw)
-    ea.tree.slot(period, read)
-    for _ in range(2):
-        noise = [torch.randn(n, generator=g0).to(DEV) * 1e-3 for n in sizes]
-        for p, q, z in zip(pa, pb, noise):
-            p.add_(z)
-            q.add_(z)
-        ea.step()
-        eb.step()
-        torch.cuda.synchronize()
-        assert torch.equal(ea.theta.view(torch.int32), eb.theta.view(torch.int32))
-        assert torch.equal(ea.mom.view(torch.int32), eb.mom.view(torch.int32))
-        if ea.wire is not None and kernel != "delta_sgd":
-            assert torch.equal(ea.wire.view(torch.int32), eb.wire.view(torch.int32))
-        for p, q in zip(pa, pb):
-            assert torch.equal(p.view(torch.int32), q.view(torch.int32))
-    with pytest.raises(_lib.DilocoHipError, match="period"):
-        ea.tree.slot(100, 100)
-    ea.close()
-    eb.close()
-
-
 @pytest.mark.parametrize("kernel", ["delta_pack_sgd", "delta_pack_sgd_bf16", "delta_sgd",
                                     "two_kernel", "two_kernel_bf16"])
 @pytest.mark.parametrize("misaligned", [False, True])
 def test_store_policies_are_bit_identical(kernel, misaligned):
-    """dl_tree_tune's store policies (plain, non-temporal, write-through sc1 buffer stores, both
-    flags) change only the timing: θ, momentum, the wire (fp32 and bf16) and the inner params
-    equal the AUTO policy's bit for bit, ragged tails and the 4-B-aligned scalar path included."""
+    """dl_tree_tune's store policies in the product library (plain and non-temporal stores
+    after non-temporal loads) change only the timing: θ, momentum, the wire (fp32 and bf16)
+    and the inner params equal the AUTO policy's bit for bit, ragged tails and the 4-B-aligned
+    scalar path included. The tuning-only policies (plain loads, write-through for every
+    kernel: make TUNING=1) are refused by the product library."""
     sizes = RAGGED + [300 * 4096 + 77]
     g0 = torch.Generator().manual_seed(37)
     host = [torch.randn(n, generator=g0) for n in sizes]
@@ -419,9 +370,15 @@ def test_store_policies_are_bit_identical(kernel, misaligned):
           "two_kernel": dict(fuse_single=False, tile_chunks=0, wire_dtype=wire)}[
               kernel.replace("_bf16", "")]
     NTL, NTS, WT = _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_WT_STORES
-    policies = [NTL, NTL | NTS, NTL | WT, NTL | NTS | WT, WT]
+    policies = [NTL, NTL | NTS]
+    if _lib.load().dl_tuning_build():
+        policies += [NTL | WT, NTL | NTS | WT, WT, 0, NTS]
     ref_p = place()
     ref = OuterSync(ref_p, world_size=1, **kw)
+    if not _lib.load().dl_tuning_build():
+        for f in (NTL | WT, WT, 0, NTS):
+            with pytest.raises(_lib.DilocoHipError, match="TUNING"):
+                ref.tree.tune(0, f)
     runs = []
     for f in policies:
         p = place()
@@ -939,3 +896,38 @@ def test_peer_gather_copies_every_source():
                   each, dst.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert torch.equal(dst, torch.cat(srcs)), (nsrc, each)
+
+
+def test_slot_rebound_on_another_stream_waits_for_the_first_streams_work():
+    """A slot bound and used on stream A, then rebound to other tensors and used on stream B
+    with no ordering by the caller: B's bind waits for A's kernel (the per-slot event), so
+    A's kernel reads the first binding and B's the second (dl_tree_bind)."""
+    from diloco_amd.kernels import HipKernels
+
+    k = HipKernels()
+    sizes = [4096 * 2048 + 5, 777, 4096 * 1024]  # ~12.6 M elements: A's kernel runs a while
+    tree = k.tree(sizes, torch.device(DEV))
+    g = torch.Generator().manual_seed(7)
+    theta = torch.randn(tree.total, generator=g).to(DEV)
+    xs = [torch.randn(n, generator=g).to(DEV) for n in sizes]
+    ys = [torch.randn(n, generator=g).to(DEV) for n in sizes]
+    wa = torch.empty(tree.total, device=DEV)
+    wb = torch.empty(tree.total, device=DEV)
+    sa, sb = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        with torch.cuda.stream(sa):
+            tree.bind(SLOT_INNER, xs, sa.cuda_stream)
+            for _ in range(4):  # keep stream A busy reading the first binding
+                k.delta_pack(tree, _lib.ALL_BUCKETS, SLOT_INNER, theta, wa)
+        tree._bound[SLOT_INNER] = None  # force the rebind through the C-ABI
+        with torch.cuda.stream(sb):
+            tree.bind(SLOT_INNER, ys, sb.cuda_stream)
+            k.delta_pack(tree, _lib.ALL_BUCKETS, SLOT_INNER, theta, wb)
+        torch.cuda.synchronize()
+        tree._bound[SLOT_INNER] = None
+        for t, (o, n) in enumerate(zip(tree.seg_off[:-1], sizes)):
+            th = theta[int(o):int(o) + n]
+            assert torch.equal(wa[int(o):int(o) + n], th - xs[t]), t
+            assert torch.equal(wb[int(o):int(o) + n], th - ys[t]), t
+    tree.close()

@@ -133,3 +133,136 @@ def test_sync_write_back_is_the_default_and_argument_errors():
     assert not outer._diloco_mirror.deferred
     with pytest.raises(ValueError, match="write_back"):
         get_outer_model(inner, write_back="lazy")
+
+
+# ---- the fused device outer model (mirror.DeviceOuterMirror, fused=True) ---------------------
+class _Counting(OracleKernels):
+    """The checker backend, counting the calls the mirror makes."""
+
+    def __init__(self):
+        self.calls = {}
+        self._depth = 0
+        for name in ("delta_pack", "delta_pack_sgd", "unpack_sgd", "unpack_avg", "scatter"):
+            def wrap(*a, _n=name, _f=getattr(OracleKernels, name), **kw):
+                if self._depth == 0:  # the mirror's launches, not the checker's own helpers
+                    self.calls[_n] = self.calls.get(_n, 0) + 1
+                self._depth += 1
+                try:
+                    return _f(self, *a, **kw)
+                finally:
+                    self._depth -= 1
+            setattr(self, name, wrap)
+
+
+def _device_models(fused):
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.from_numpy(v.copy()).view(s))
+                                       for v, s in zip(theta0, shapes)])
+    outer = get_outer_model(inner, placement="device", fused=fused)
+    return inner, outer
+
+
+@pytest.mark.parametrize("quiet", [True, False])
+def test_fused_device_model_matches_reference_one_peer(quiet):
+    """src/train.py:263-269 at one peer: quiet (nothing read between the calls) runs ONE
+    dl_delta_pack_sgd per outer step and no scatter; reading .grad mid-sequence computes the
+    delta first. Both bit-exact vs the reference (micro_n1.npz), .grad included."""
+    from diloco_amd.mirror import OuterParameter
+
+    k = _Counting()
+    kernels.set_default_kernels(k)
+    g = load_npz("micro_n1.npz")
+    inner, outer = _device_models(True)
+    assert all(isinstance(p, OuterParameter) for p in outer.parameters())
+    opt = get_optimizer(outer, SGD_CFG)
+    for s in (1, 2):
+        _set_inner(inner, outer, s)
+        k.calls.clear()
+        compute_pseudo_gradient(inner, outer)
+        if not quiet:
+            assert _host(p.grad for p in outer.parameters()).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        # sync_gradients at one peer returns at once (src/comm.py:118-119)
+        opt.step()
+        sync_inner_model(outer, inner)
+        if quiet:
+            assert k.calls == {"delta_pack_sgd": 1}, k.calls
+        else:
+            assert k.calls == {"delta_pack": 1, "unpack_sgd": 1}, k.calls
+        assert _host(outer.parameters()).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert _host(p.grad for p in outer.parameters()).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        assert _host(opt.state[p]["momentum_buffer"]
+                     for p in outer.parameters()).tobytes() == g[f"buf_s{s}"].tobytes()
+        assert _host(inner.parameters()).tobytes() == g[f"theta_s{s}"].tobytes()
+
+
+def test_fused_sync_inner_model_rescatters_when_either_side_changed():
+    k = _Counting()
+    kernels.set_default_kernels(k)
+    inner, outer = _device_models(True)
+    opt = get_optimizer(outer, SGD_CFG)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    opt.step()
+    p0 = next(outer.parameters())
+    with torch.no_grad():
+        p0.add_(0.5)  # θ changed after the fused write: the inner params must get it
+    k.calls.clear()
+    sync_inner_model(outer, inner)
+    assert k.calls == {"scatter": 1}
+    assert _host(inner.parameters()).tobytes() == _host(outer.parameters()).tobytes()
+    k.calls.clear()
+    sync_inner_model(outer, inner)  # nothing changed since: verified no-op
+    assert k.calls == {}
+    with torch.no_grad():
+        next(inner.parameters()).mul_(2.0)  # the inner side changed
+    sync_inner_model(outer, inner)
+    assert k.calls == {"scatter": 1}
+    assert _host(inner.parameters()).tobytes() == _host(outer.parameters()).tobytes()
+
+
+def test_fused_inner_modified_before_use_is_an_error_and_eager_mode_is_the_reference():
+    inner, outer = _device_models(True)
+    opt = get_optimizer(outer, SGD_CFG)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    with torch.no_grad():
+        next(inner.parameters()).add_(1.0)
+    with pytest.raises(RuntimeError, match="DILOCO_OUTER_FUSED=0"):
+        opt.step()
+    # eager: every call computes at once; the same modification is simply not seen
+    g = load_npz("micro_n1.npz")
+    inner, outer = _device_models(False)
+    assert not outer._diloco_mirror.fused
+    opt = get_optimizer(outer, SGD_CFG)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    with torch.no_grad():
+        next(inner.parameters()).add_(1.0)
+    opt.step()
+    sync_inner_model(outer, inner)
+    assert _host(outer.parameters()).tobytes() == g["theta_s1"].tobytes()
+    assert _host(inner.parameters()).tobytes() == g["theta_s1"].tobytes()
+
+
+def test_fused_outer_model_pickles_and_deepcopies_as_plain_parameters():
+    import copy
+    import io
+
+    inner, outer = _device_models(True)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    buf = io.BytesIO()
+    torch.save(outer.state_dict(), buf)
+    c = copy.deepcopy(outer)
+    assert all("_dl_mirror" not in p.__dict__ for p in c.parameters())
+    assert _host(c.parameters()).tobytes() == _host(outer.parameters()).tobytes()
+    # a stock torch SGD on the fused model reads .grad (the pending delta is computed first)
+    g = load_npz("micro_n1.npz")
+    sgd = torch.optim.SGD(outer.parameters(), lr=0.7, momentum=0.9, nesterov=True)
+    sgd.step()
+    sync_inner_model(outer, inner)
+    assert _host(outer.parameters()).tobytes() == g["theta_s1"].tobytes()
+    assert _host(inner.parameters()).tobytes() == g["theta_s1"].tobytes()

@@ -7,7 +7,9 @@ every timed launch, variants interleaved round by round in one process (cdna_hip
     python tools/cold_sweep.py [--tree t125] [--rounds 11] [--out x.json] [--what flags,tiles]
 
 flags : dl_tree_tune launch policy (NT loads / NT or write-through stores) of dl_delta_pack, dl_unpack_sgd,
-        dl_delta_sgd one launch over the whole tree each
+        dl_delta_sgd one launch over the whole tree each. Plain loads and write-through stores
+        exist only in the tuning build: make -C diloco-swarm_amd/csrc TUNING=1, then run with
+        DILOCO_HIP_LIB=diloco-swarm_amd/lib/libdiloco_hip_tuning.so
 tiles : the one-replica two-kernel step (dl_pack_sgd_tiled) at tile sizes 0 (whole-range
         launches), 1024 ... 16384 chunks, against the one-pass dl_delta_sgd
 """
