@@ -301,7 +301,8 @@ DL_API int dl_tree_bucket_chunks(dl_tree_t t, int32_t b, int32_t* c0, int32_t* c
 
 DL_API int dl_tree_tune(dl_tree_t t, int32_t max_blocks, int32_t flags) {
   if (!t || max_blocks < 0) return fail(DL_E_ARG, "dl_tree_tune: bad argument");
-  if (flags != DL_TUNE_AUTO && (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES | DL_TUNE_WT_STORES)))
+  if (flags != DL_TUNE_AUTO &&
+      (flags & ~(DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES | DL_TUNE_WT_STORES | DL_TUNE_PAIRS)))
     return fail(DL_E_ARG, "dl_tree_tune: unknown flags 0x%x", flags);
 #ifndef DL_TUNING
   // the product build instantiates the AUTO policies only: NT loads, plain or NT stores
@@ -398,6 +399,11 @@ constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // write-through only for the int8 unpack below 2^28 elements.
 constexpr int32_t kAutoWT = DL_TUNE_NT_LOADS | DL_TUNE_WT_STORES;
 enum class Big { keep, nt_stores, nt_stores_2 };
+// dl_delta_pack / dl_gather: two chunks per workgroup under AUTO (DL_TUNE_PAIRS)
+#ifndef DL_AUTO_PAIRS
+#define DL_AUTO_PAIRS 0
+#endif
+constexpr bool kAutoPairs = DL_AUTO_PAIRS != 0;
 
 int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who,
                 int32_t auto_flags = kAutoOther, Big big = Big::keep) {
@@ -417,6 +423,7 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
   L->nchunk = int32_t(t->chunks.size());
   L->grid = t->grid;
   L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
+  L->pairs = (L->flags & DL_TUNE_PAIRS) != 0;
   if (t->flags == DL_TUNE_AUTO && big != Big::keep && L->c1 - L->c0 >= kBigLaunchChunks) {
     L->flags = (L->flags & ~DL_TUNE_WT_STORES) | DL_TUNE_NT_STORES;  // WT -> NT above 2^28
     if (big == Big::nt_stores_2 && L->grid == 0) L->grid = (L->c1 - L->c0 + 1) / 2;
@@ -456,7 +463,8 @@ extern "C" {
 DL_API int dl_delta_pack(dl_tree_t t, int32_t b, int32_t inner_slot, const float* outer,
                          void* wire, int32_t wire_dtype, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack", kAutoDelta, Big::nt_stores));
+  DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack", kAutoDelta | (kAutoPairs ? DL_TUNE_PAIRS : 0),
+                     Big::nt_stores));
   DL_TRY(check_slot(t, inner_slot, "dl_delta_pack"));
   DL_TRY(check_packed(outer, "dl_delta_pack", "outer"));
   DL_TRY(check_packed(wire, "dl_delta_pack", "wire"));
@@ -833,7 +841,8 @@ DL_API int dl_unpack_sgd_q8(dl_tree_t t, int32_t b, const void* slots, float* ou
 DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int32_t dtype,
                      dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_gather", kAutoOther, Big::nt_stores));
+  DL_TRY(make_launch(t, b, s, &L, "dl_gather", kAutoOther | (kAutoPairs ? DL_TUNE_PAIRS : 0),
+                     Big::nt_stores));
   DL_TRY(check_slot(t, src_slot, "dl_gather"));
   DL_TRY(check_packed(packed, "dl_gather", "packed"));
   DL_TRY(check_dtype(dtype, "dl_gather"));

@@ -184,6 +184,33 @@ hipError_t launch_walk(const Launch& L, const Body& body, int32_t grid) {
   return hipGetLastError();
 }
 
+// The pair walker: workgroup i takes chunks 2i and 2i+1 of the range (run2 issues both
+// chunks' loads before any store); a last odd chunk goes through run. Grid = ceil(n / 2), or
+// the tree's cap with a grid-stride over pairs.
+template <class Body, bool NTL, int NTS>
+__global__ void __launch_bounds__(kThreads)
+    k_walk_pairs(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1,
+                 void* const* __restrict__ caddr, int32_t nchunk, Body body) {
+  const int32_t n = c1 - c0;
+  for (int32_t i = 2 * int32_t(blockIdx.x); i < n; i += 2 * int32_t(gridDim.x)) {
+    const int32_t c = c0 + i;
+    const Chunk k0 = chunks[c];
+    if (i + 1 < n) {
+      const Chunk k1 = chunks[c + 1];
+      body.template run2<NTL, NTS>(k0, c, k1, c + 1, caddr, nchunk, int(threadIdx.x));
+    } else {
+      body.template run<NTL, NTS>(k0, c, caddr, nchunk, int(threadIdx.x));
+    }
+  }
+}
+
+template <class Body, bool NTL, int NTS>
+hipError_t launch_pairs(const Launch& L, const Body& body, int32_t grid) {
+  hipLaunchKernelGGL((k_walk_pairs<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream,
+                     L.chunks, L.c0, L.c1, L.caddr, L.nchunk, body);
+  return hipGetLastError();
+}
+
 // bodies whose AUTO policy stores write-through declare kWriteThrough = true
 template <class B, class = void>
 struct write_through : std::false_type {};
@@ -214,6 +241,18 @@ hipError_t run(const Launch& L, const Body& body) {
 #endif
   if (sp == kStNT) return launch_walk<Body, true, kStNT>(L, body, grid);
   return launch_walk<Body, true, kStPlain>(L, body, grid);
+}
+
+// run() for a pair-capable body (DeltaPackPair, GatherPair): NT loads, plain / NT stores
+template <class Body>
+hipError_t run_pairs(const Launch& L, const Body& body) {
+  const int32_t n = L.c1 - L.c0;
+  if (n <= 0) return hipSuccess;
+  const int32_t np = (n + 1) / 2;
+  const int32_t grid = (L.grid > 0 && L.grid < np) ? L.grid : np;
+  if (!(L.flags & DL_TUNE_NT_LOADS) || (L.flags & DL_TUNE_WT_STORES)) return run(L, body);
+  if (L.flags & DL_TUNE_NT_STORES) return launch_pairs<Body, true, kStNT>(L, body, grid);
+  return launch_pairs<Body, true, kStPlain>(L, body, grid);
 }
 
 }  // namespace

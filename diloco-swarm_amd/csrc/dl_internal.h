@@ -39,6 +39,7 @@ struct Launch {
   int32_t grid;   // 0 = one workgroup per chunk
   int32_t flags;  // DL_TUNE_*
   hipStream_t stream;
+  bool pairs;  // two chunks per workgroup, loads of both before the stores (run_pairs)
 };
 
 // peers of the direct exchange (dl_xgmi.hip): each rank's packed wire and θ, IPC-mapped

@@ -57,6 +57,62 @@ struct DeltaPack {
   }
 };
 
+// Two chunks per workgroup, every load of both issued before the first store: 8 float4 per
+// lane per input stream in flight instead of 4 (the 2-read / 1-write kernels are latency-bound
+// at 4: SQ_WAIT_ANY / SQ_WAVE_CYCLES 0.6 vs 0.3 for the SGD kernels). Used by
+// dl_delta_pack and dl_gather under DL_TUNE_AUTO (run_pairs). A misaligned tensor (the
+// scalar path) takes the one-chunk body for both chunks.
+template <typename W>
+struct DeltaPackPair {
+  DeltaPack<W> one;
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    one.template run<NTL, NTS>(ck, c, caddr, nchunk, tid);
+  }
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run2(const Chunk& k0, int c0, const Chunk& k1, int c1,
+                                       void* const* caddr, int nchunk, int tid) const {
+    const float* in0 = slot_ptr<const float>(caddr, nchunk, one.inner_slot, c0);
+    const float* in1 = slot_ptr<const float>(caddr, nchunk, one.inner_slot, c1);
+    if (!aligned16(in0) || !aligned16(in1)) {
+      run<NTL, NTS>(k0, c0, caddr, nchunk, tid);
+      run<NTL, NTS>(k1, c1, caddr, nchunk, tid);
+      return;
+    }
+    const float* th0 = one.outer + k0.poff;
+    const float* th1 = one.outer + k1.poff;
+    const int nv0 = k0.len >> 2, nv1 = k1.len >> 2;
+    float4 a0[kUnroll], b0[kUnroll], a1[kUnroll], b1[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + tid;
+      if (v < nv0) {
+        a0[u] = ldf4<NTL>(th0, v);
+        b0[u] = ldf4<NTL>(in0, v);
+      }
+      if (v < nv1) {
+        a1[u] = ldf4<NTL>(th1, v);
+        b1[u] = ldf4<NTL>(in1, v);
+      }
+    }
+    W* w0 = one.wire + k0.poff;
+    W* w1 = one.wire + k1.poff;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + tid;
+      if (v < nv0) WireIO<W>::template st4<NTS>(w0, v, sub4(a0[u], b0[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + tid;
+      if (v < nv1) WireIO<W>::template st4<NTS>(w1, v, sub4(a1[u], b1[u]));
+    }
+    const int i0 = (nv0 << 2) + tid, i1 = (nv1 << 2) + tid;
+    if (i0 < k0.len) WireIO<W>::st1(w0, i0, th0[i0] - in0[i0]);
+    if (i1 < k1.len) WireIO<W>::st1(w1, i1, th1[i1] - in1[i1]);
+  }
+};
+
 // a3 unpack: dst = wire / d
 template <typename W, bool DIV>
 struct UnpackAvg {
@@ -324,6 +380,49 @@ struct Gather {
   }
 };
 
+template <typename W>
+struct GatherPair {
+  Gather<W> one;
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
+    one.template run<NTL, NTS>(ck, c, caddr, nchunk, tid);
+  }
+  template <bool NTL, int NTS>
+  __device__ __forceinline__ void run2(const Chunk& k0, int c0, const Chunk& k1, int c1,
+                                       void* const* caddr, int nchunk, int tid) const {
+    const float* s0 = slot_ptr<const float>(caddr, nchunk, one.src_slot, c0);
+    const float* s1 = slot_ptr<const float>(caddr, nchunk, one.src_slot, c1);
+    if (!aligned16(s0) || !aligned16(s1)) {
+      run<NTL, NTS>(k0, c0, caddr, nchunk, tid);
+      run<NTL, NTS>(k1, c1, caddr, nchunk, tid);
+      return;
+    }
+    const int nv0 = k0.len >> 2, nv1 = k1.len >> 2;
+    float4 x0[kUnroll], x1[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + tid;
+      if (v < nv0) x0[u] = ldf4<NTL>(s0, v);
+      if (v < nv1) x1[u] = ldf4<NTL>(s1, v);
+    }
+    W* p0 = one.packed + k0.poff;
+    W* p1 = one.packed + k1.poff;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + tid;
+      if (v < nv0) WireIO<W>::template st4<NTS>(p0, v, x0[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int v = u * kThreads + tid;
+      if (v < nv1) WireIO<W>::template st4<NTS>(p1, v, x1[u]);
+    }
+    const int i0 = (nv0 << 2) + tid, i1 = (nv1 << 2) + tid;
+    if (i0 < k0.len) WireIO<W>::st1(p0, i0, s0[i0]);
+    if (i1 < k1.len) WireIO<W>::st1(p1, i1, s1[i1]);
+  }
+};
+
 // packed fp32 -> per-tensor fp32
 struct Scatter {
   const float* packed;
@@ -574,9 +673,12 @@ hipError_t launch_probe(bool write, int streams, const void* src, void* dst, int
 
 hipError_t launch_delta_pack(const Launch& L, int inner_slot, const float* outer, void* wire,
                              int wire_dtype) {
-  if (wire_dtype == DL_BF16)
-    return run(L, DeltaPack<bf16_t>{inner_slot, outer, static_cast<bf16_t*>(wire)});
-  return run(L, DeltaPack<float>{inner_slot, outer, static_cast<float*>(wire)});
+  if (wire_dtype == DL_BF16) {
+    const DeltaPack<bf16_t> one{inner_slot, outer, static_cast<bf16_t*>(wire)};
+    return L.pairs ? run_pairs(L, DeltaPackPair<bf16_t>{one}) : run(L, one);
+  }
+  const DeltaPack<float> one{inner_slot, outer, static_cast<float*>(wire)};
+  return L.pairs ? run_pairs(L, DeltaPackPair<float>{one}) : run(L, one);
 }
 
 template <typename W>
@@ -805,8 +907,12 @@ hipError_t launch_delta_pack_sgd(const Launch& L, int inner_slot, float* outer, 
 }
 
 hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype) {
-  if (dtype == DL_BF16) return run(L, Gather<bf16_t>{src_slot, static_cast<bf16_t*>(packed)});
-  return run(L, Gather<float>{src_slot, static_cast<float*>(packed)});
+  if (dtype == DL_BF16) {
+    const Gather<bf16_t> one{src_slot, static_cast<bf16_t*>(packed)};
+    return L.pairs ? run_pairs(L, GatherPair<bf16_t>{one}) : run(L, one);
+  }
+  const Gather<float> one{src_slot, static_cast<float*>(packed)};
+  return L.pairs ? run_pairs(L, GatherPair<float>{one}) : run(L, one);
 }
 
 hipError_t launch_scatter(const Launch& L, const float* packed, int dst_slot) {

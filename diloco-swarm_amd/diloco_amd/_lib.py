@@ -23,7 +23,7 @@ MAX_SLOTS = 4
 Q8_SLOT_BYTES = 4160
 IPC_HANDLE_BYTES = 64
 DL_F32, DL_BF16, DL_F16, DL_U8 = 0, 1, 2, 3
-TUNE_NT_LOADS, TUNE_NT_STORES, TUNE_WT_STORES = 1, 2, 8
+TUNE_NT_LOADS, TUNE_NT_STORES, TUNE_WT_STORES, TUNE_PAIRS = 1, 2, 8, 16
 TUNE_AUTO = -1
 COPY_WIDE, COPY_READ, COPY_WRITE = 8, 16, 32
 

@@ -54,8 +54,12 @@ class HipKernels:
         with torch.cuda.device(device):
             return PackedTree(numels, cap_elems, bucket_align)
 
-    def bind(self, tree: PackedTree, slot: int, tensors: Sequence[torch.Tensor], device) -> None:
-        tree.bind(slot, tensors, torch.cuda.current_stream(device).cuda_stream)
+    def bind(self, tree: PackedTree, slot: int, tensors: Sequence[torch.Tensor], device,
+             key=None) -> None:
+        """key: tuple of the tensors' addresses, if the caller computed it (skips a pass)."""
+        if key is not None and tree._bound[slot] == key:
+            return
+        tree.bind(slot, tensors, torch.cuda.current_stream(device).cuda_stream, key)
 
     def delta_pack(self, tree, bucket, inner_slot, theta, wire) -> None:
         _lib.call("dl_delta_pack", tree.handle, bucket, inner_slot, theta.data_ptr(),

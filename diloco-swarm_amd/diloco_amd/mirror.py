@@ -304,15 +304,34 @@ class HostOuterMirror:
 
 
 
-# The C-level `.grad` of every tensor: the mirror reads and assigns it through this
-# descriptor, bypassing OuterParameter's property (no recursion, no per-access Python call).
+# The C-level `.grad` / `.data` of every tensor: the mirror reads and assigns them through
+# these descriptors, bypassing OuterParameter's properties (no recursion, no extra Python call).
 _GRAD = torch._C.TensorBase.grad
+_DATA = torch._C.TensorBase.data
 
 
-def _sig(ts: Sequence[torch.Tensor]) -> tuple:
-    """Storage address and version counter of every tensor: any in-place torch write or a
-    replaced `.data` changes it (kernel writes through the packed arenas do not)."""
-    return tuple((t.data_ptr(), t._version) for t in ts)
+def _ptrs(ts: Sequence[torch.Tensor]) -> List[int]:
+    return [t.data_ptr() for t in ts]
+
+
+def _vers(ts: Sequence[torch.Tensor]) -> List[int]:
+    """Version counters: any in-place torch write bumps them (kernel writes through the packed
+    arenas and writes through `.data` do not)."""
+    return [t._version for t in ts]
+
+
+def module_params(model: torch.nn.Module) -> List[torch.nn.Parameter]:
+    """list(model.parameters()), same order (modules in named_modules() order, each module's
+    parameters in registration order, a shared parameter at its first occurrence), with the
+    duplicates found by identity instead of Tensor.__hash__ (a Python call per lookup: the
+    per-call cost of the drop-in functions on a 148-tensor tree)."""
+    seen, out = set(), []
+    for mod in model.modules():
+        for p in mod._parameters.values():
+            if p is not None and id(p) not in seen:
+                seen.add(id(p))
+                out.append(p)
+    return out
 
 
 class OuterParameter(torch.nn.Parameter):
@@ -322,46 +341,52 @@ class OuterParameter(torch.nn.Parameter):
     delta instead of computing it, and sync_gradients leaves the packed .grad holding the Σ
     with the /n pending, so the outer SGD can run all of it in one pass. Reading or assigning
     `.grad` first completes whatever is pending, so every value a caller observes equals the
-    reference's (src/utils.py:221, src/comm.py:122-123)."""
+    reference's (src/utils.py:221, src/comm.py:122-123). Assigning `.grad` or `.data` also
+    tells the mirror that its packed views may have been replaced, so a step in which nobody
+    assigned them skips the per-tensor address checks."""
 
-    def _settle(self) -> None:
+    def _mirror(self):
         r = self.__dict__.get("_dl_mirror")
-        m = r() if r is not None else None
-        if m is not None and m.pending:
-            m.settle_grads()
+        return r() if r is not None else None
 
     @property
     def grad(self):
-        self._settle()
+        m = self._mirror()
+        if m is not None and m.pending:
+            m.settle_grads()
         return _GRAD.__get__(self)
 
     @grad.setter
     def grad(self, value):
-        self._settle()
+        m = self._mirror()
+        if m is not None:
+            if m.pending:
+                m.settle_grads()
+            m.grads_touched = True
         _GRAD.__set__(self, value)
 
     @grad.deleter
     def grad(self):
-        self._settle()
+        m = self._mirror()
+        if m is not None:
+            if m.pending:
+                m.settle_grads()
+            m.grads_touched = True
         _GRAD.__delete__(self)
+
+    @property
+    def data(self):
+        return _DATA.__get__(self)
+
+    @data.setter
+    def data(self, value):
+        m = self._mirror()
+        if m is not None:
+            m.theta_touched = True
+        _DATA.__set__(self, value)
 
     def __reduce_ex__(self, proto):  # pickles as a plain Parameter (the mirror stays behind)
         return (torch._utils._rebuild_parameter, (self.data, self.requires_grad, OrderedDict()))
-
-
-def use_outer_parameters(model: torch.nn.Module) -> None:
-    """Replace every parameter of `model` by an OuterParameter over the same data (shared
-    parameters stay shared). Only for a module nothing else references yet: get_outer_model's
-    fresh deep copy."""
-    memo = {}
-    for mod in model.modules():
-        for name, p in list(mod._parameters.items()):
-            if p is None or isinstance(p, OuterParameter):
-                continue
-            q = memo.get(id(p))
-            if q is None:
-                q = memo[id(p)] = OuterParameter(p.data, p.requires_grad)
-            mod._parameters[name] = q
 
 
 class DeviceOuterMirror:
@@ -374,29 +399,30 @@ class DeviceOuterMirror:
 
     fused=False (eager) runs every call as the reference does, one kernel each:
         dl_delta_pack -> RCCL all_reduce + dl_unpack_avg -> dl_unpack_sgd -> dl_scatter
-        = 12 + (8) + 20 + 8 B per parameter (44 at N > 1, 40 at one peer).
+        = 12 + (8) + 20 + 8 B per parameter (48 at N > 1, 40 at one peer).
     fused=True (the default for this placement, DILOCO_OUTER_FUSED=0 turns it off) keeps the
     observable values and runs the sequence in as few HBM passes as the data flow allows:
-      - compute_pseudo_gradient records the delta (inner params, their signature);
+      - compute_pseudo_gradient records the delta (inner params, their addresses and version
+        counters) instead of computing it;
       - sync_gradients packs each bucket just before its RCCL all_reduce and leaves the /n
         pending (the packed .grad holds the Σ);
       - OuterSGD.step runs ONE pass: at one peer dl_delta_pack_sgd (delta, .grad, SGD, θ and
         the inner params: 28 B/param, the engine's headline kernel); at N > 1 dl_unpack_sgd with
         the divisor and the inner write (24 B after the 12 B pack);
-      - sync_inner_model verifies that the inner params still hold θ (same tensors, same
-        storage, no version bump on either side since that write) and does nothing; anything
+      - sync_inner_model verifies that the inner params still hold θ (same tensors at the same
+        addresses, no version bump on either side since that write) and does nothing; anything
         else -> dl_scatter as in eager mode.
     Reading or assigning an outer parameter's .grad completes the pending work first
     (OuterParameter), so .grad always shows the reference's value. Two consequences differ from
     the reference and are the price of the fusion: the inner params receive θ_new during
     OuterSGD.step() rather than in sync_inner_model (train.py reads neither in between), and
     changing the inner params or θ in place between compute_pseudo_gradient and the call that
-    consumes the delta raises instead of being silently used (writes through `.data` bypass
-    version counters: call invalidate() after them)."""
+    consumes the delta raises instead of being silently used (writes through an inner tensor's
+    `.data` bypass version counters: call invalidate() after them)."""
 
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
                  bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = False):
-        self.params: List[torch.nn.Parameter] = list(outer_model.parameters())
+        self.params: List[torch.nn.Parameter] = module_params(outer_model)
         if not self.params:
             raise ValueError("outer model has no parameters")
         self.k = kernels or default_kernels()
@@ -406,9 +432,6 @@ class DeviceOuterMirror:
                 raise ValueError(f"outer parameter {i} is on {p.device}, expected {self.device}")
             if p.dtype != torch.float32:
                 raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
-        if fused and not all(isinstance(p, OuterParameter) for p in self.params):
-            raise TypeError("fused=True needs OuterParameter parameters (use_outer_parameters): "
-                            "their .grad completes the deferred work")
         self.fused = fused
         self.numels = [p.numel() for p in self.params]
         self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems)
@@ -422,16 +445,45 @@ class DeviceOuterMirror:
         self._views = {"theta": self._make_views(self.d_theta),
                        "wire": self._make_views(self.d_wire)}
         self._ptrs = {k: [v.data_ptr() for v in vs] for k, vs in self._views.items()}
-        self._relay("theta", "data")
-        # fused-mode state
-        self._delta = None   # pending pseudo-gradient: (inner params, their _sig, θ versions)
-        self._div = 1        # pending /n: d_wire holds the Σ of the peers' deltas
-        self._target = None  # (inner params, _sig) of the last compute_pseudo_gradient
-        self._synced = None  # (inner params, _sig, θ versions) when the inner params hold θ
+        # fused mode: OuterParameter flags assignments of .grad / .data, so the address checks
+        # run only after one (or after a version bump on θ)
+        self.theta_touched = True
+        self.grads_touched = True
+        self._theta_ver = None
+        self._relay_theta()
         if fused:
-            ref = weakref.ref(self)
-            for p in self.params:
-                p.__dict__["_dl_mirror"] = ref
+            self._install_outer_parameters(outer_model)
+        self._delta = None   # pending pseudo-gradient: (inner params, ptrs, versions, θ versions)
+        self._div = 1        # pending /n: d_wire holds the Σ of the peers' deltas
+        self._target = None  # (inner params, ptrs, versions) of the last compute_pseudo_gradient
+        self._synced = None  # (inner params, ptrs, versions, θ versions): inner holds θ
+        self._mom_src: Optional[List[torch.Tensor]] = None  # the buffers the last step returned
+    def _install_outer_parameters(self, model: torch.nn.Module) -> None:
+        """Fused mode: every parameter of the outer model becomes an OuterParameter created
+        over its view of the θ arena (shared parameters stay shared). A tensor made from a view
+        shares its base's version counter, so every in-place write to any outer parameter
+        bumps d_theta's one counter: the per-call check that θ is unchanged reads one integer
+        instead of 148 (or 292) version counters."""
+        index = {id(p): i for i, p in enumerate(self.params)}
+        new: List[Optional[OuterParameter]] = [None] * len(self.params)
+        ref = weakref.ref(self)
+        for mod in model.modules():
+            for name, p in list(mod._parameters.items()):
+                if p is None:
+                    continue
+                i = index[id(p)]
+                if new[i] is None:
+                    q = OuterParameter(self._views["theta"][i], p.requires_grad)
+                    q.__dict__["_dl_mirror"] = ref
+                    new[i] = q
+                mod._parameters[name] = new[i]
+        self.params = new
+        self._theta_ver = self._theta_version()
+
+    def _theta_version(self):
+        """fused: d_theta's version counter, shared by every outer parameter (one integer);
+        eager: the parameters' own counters."""
+        return self.d_theta._version if self.fused else _vers(self.params)
 
     def _make_views(self, arena: torch.Tensor) -> List[torch.Tensor]:
         return [arena[o:o + n].view(p.shape)
@@ -444,7 +496,7 @@ class DeviceOuterMirror:
     def _in_place(self, kind: str, what: str) -> bool:
         exp = self._ptrs[kind]
         if what == "data":
-            return all(p.data_ptr() == e for p, e in zip(self.params, exp))
+            return _ptrs(self.params) == exp
         for p, e in zip(self.params, exp):
             g = _GRAD.__get__(p)
             if g is None or g.data_ptr() != e:
@@ -460,7 +512,7 @@ class DeviceOuterMirror:
         with torch.no_grad():
             for i, p in enumerate(self.params):
                 v = views[i]
-                cur = p.data if what == "data" else _GRAD.__get__(p)
+                cur = _DATA.__get__(p) if what == "data" else _GRAD.__get__(p)
                 if cur is not None and cur.data_ptr() == v.data_ptr():
                     continue
                 if cur is None:
@@ -472,41 +524,58 @@ class DeviceOuterMirror:
                 else:
                     v.copy_(cur)
                 if what == "data":
-                    p.data = v
+                    _DATA.__set__(p, v)
                 else:
                     _GRAD.__set__(p, v)
         return True
 
-    def _relay_theta(self) -> None:
-        if self._relay("theta", "data"):
-            self._synced = None  # θ's arena content changed: the inner params no longer hold it
+    def _relay_theta(self, ver=None):
+        """θ's packed arena holds every outer parameter (relayed if one was replaced); returns
+        θ's version (_theta_version; `ver`: read by the caller just before). Skips the address
+        checks in fused mode when no `.data` was assigned and the version did not move since
+        the last call."""
+        if ver is None:
+            ver = self._theta_version()
+        if not self.fused or self.theta_touched or ver != self._theta_ver:
+            if self._relay("theta", "data"):
+                self._synced = None  # θ's arena content changed: the inner no longer holds it
+                ver = self._theta_version()  # the relay's own copies bumped it
+            self.theta_touched = False
+            self._theta_ver = ver
+        return ver
 
-    def _theta_versions(self) -> tuple:
-        return tuple(p._version for p in self.params)
+    def _relay_grads(self, zero_fill_missing: bool) -> None:
+        if not self.fused or self.grads_touched:
+            self._relay("wire", "grad", zero_fill_missing)
+            self.grads_touched = False
 
     def invalidate(self) -> None:
-        """After writes through `.data` (no version bump): forget that the inner params hold θ."""
+        """After writes through `.data` (no version bump): forget that the inner params hold θ
+        and re-check every address at the next call."""
         self._synced = None
         self._target = None
+        self.theta_touched = self.grads_touched = True
 
     # ---- deferred work (fused mode) ------------------------------------------------------
     @property
     def pending(self) -> bool:
         return self._delta is not None or self._div != 1
 
-    def _take_delta(self) -> List[torch.Tensor]:
+    def _take_delta(self, tver_now=None) -> List[torch.Tensor]:
         """The pending delta's inner params, checked unchanged since compute_pseudo_gradient
-        and bound to SLOT_INNER."""
-        inner, isig, tver = self._delta
+        and bound to SLOT_INNER (tver_now: θ's version, if the caller has it)."""
+        inner, iptrs, ivers, tver = self._delta
         self._delta = None
-        if (_sig(inner) != isig or self._theta_versions() != tver
-                or not self._in_place("theta", "data")):
+        if tver_now is None:
+            tver_now = self._theta_version()
+        if (_ptrs(inner) != iptrs or _vers(inner) != ivers or self.theta_touched
+                or tver_now != tver):
             raise RuntimeError(
                 "the inner or the outer parameters were modified after compute_pseudo_gradient "
                 "and before the pseudo-gradient was used; the fused device outer model computes "
                 "it when it is first needed (get_outer_model(..., fused=False) or "
                 "DILOCO_OUTER_FUSED=0 computes it eagerly)")
-        self.k.bind(self.tree, SLOT_INNER, inner, self.device)
+        self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))
         return inner
 
     def settle_grads(self) -> None:
@@ -525,23 +594,25 @@ class DeviceOuterMirror:
             self.settle_grads()
 
     def _grad_views(self) -> None:
-        if not self._in_place("wire", "grad"):
+        if not self.fused or self.grads_touched:
             for p, v, e in zip(self.params, self._views["wire"], self._ptrs["wire"]):
                 g = _GRAD.__get__(p)
                 if g is None or g.data_ptr() != e:
                     _GRAD.__set__(p, v)
+            self.grads_touched = False
 
     # ---- the four reference operations --------------------------------------------------
     def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
         """outer.grad = outer - inner (src/utils.py:218-221); .grad are views of d_wire."""
         inner = list(inner_params)
-        self._relay_theta()
-        self.k.bind(self.tree, SLOT_INNER, inner, self.device)  # shape errors raise here
+        tver = self._relay_theta()
+        iptrs = _ptrs(inner)
+        self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))
         self._div = 1  # the wire is overwritten: a /n still pending is moot
         if self.fused:
-            sig = _sig(inner)
-            self._delta = (inner, sig, self._theta_versions())
-            self._target = (inner, sig)
+            ivers = _vers(inner)
+            self._delta = (inner, iptrs, ivers, tver)
+            self._target = (inner, iptrs, ivers)
         else:
             self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
         self._grad_views()
@@ -559,7 +630,7 @@ class DeviceOuterMirror:
         else:
             if self._div != 1:
                 self.settle_grads()  # a second sync_gradients reduces the averages
-            self._relay("wire", "grad", zero_fill_missing=True)
+            self._relay_grads(zero_fill_missing=True)
 
         def view(b):
             lo, hi = self.tree.bucket_ranges[b]
@@ -578,10 +649,11 @@ class DeviceOuterMirror:
                  host_bufs: Optional[List[Optional[torch.Tensor]]]) -> List[Optional[torch.Tensor]]:
         """torch.optim.SGD._single_tensor_sgd over the whole tree; returns the momentum
         buffers (views of d_mom) for the optimizer state."""
-        delta = self._take_delta() if self._delta is not None else None
-        self._relay_theta()
+        tver = self._theta_version()
+        delta = self._take_delta(tver) if self._delta is not None else None
+        tver = self._relay_theta(tver)
         if delta is None:
-            self._relay("wire", "grad", zero_fill_missing=False)
+            self._relay_grads(zero_fill_missing=False)
         first = True
         bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
         if momentum != 0:
@@ -589,31 +661,38 @@ class DeviceOuterMirror:
                 self.d_mom = torch.zeros_like(self.d_theta)
                 self._views["mom"] = self._make_views(self.d_mom)
                 self._ptrs["mom"] = [v.data_ptr() for v in self._views["mom"]]
-            have = [b is not None for b in host_bufs]
-            if any(have) and not all(have):
-                raise RuntimeError("momentum buffers exist for some outer parameters only")
-            first = not any(have)
             bufs = self._views["mom"]
-            if not first:
-                with torch.no_grad():
-                    for b, v, e in zip(host_bufs, bufs, self._ptrs["mom"]):
-                        if b.data_ptr() != e:
-                            v.copy_(b)  # e.g. a state_dict loaded into the optimizer
+            src = self._mom_src
+            if not (src is not None and len(host_bufs) == len(src)
+                    and all(a is b for a, b in zip(host_bufs, src))):
+                have = [b is not None for b in host_bufs]
+                if any(have) and not all(have):
+                    raise RuntimeError("momentum buffers exist for some outer parameters only")
+                first = not any(have)
+                if not first:
+                    with torch.no_grad():
+                        for b, v, e in zip(host_bufs, bufs, self._ptrs["mom"]):
+                            if b.data_ptr() != e:
+                                v.copy_(b)  # e.g. a state_dict loaded into the optimizer
+            else:
+                first = False  # the buffers this mirror returned last step
+            self._mom_src = bufs
         mom = self.d_mom if momentum != 0 else None
         # the inner params of the last compute_pseudo_gradient take θ_new in the same pass
-        # (fused mode), unless they were modified since
+        # (fused mode). The record of that write keeps their addresses and versions from then:
+        # if they moved or were written since, sync_inner_model sees it and scatters again
         target, self._target = self._target, None
-        write = target is not None and (delta is not None or _sig(target[0]) == target[1])
+        write = target is not None
         if delta is not None:  # one peer: the delta never leaves registers
             self.k.delta_pack_sgd(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire, mom,
                                   lr, momentum, nesterov, first)
         else:
             if write:
-                self.k.bind(self.tree, SLOT_INNER, target[0], self.device)
+                self.k.bind(self.tree, SLOT_INNER, target[0], self.device, key=tuple(target[1]))
             # a pending /n stays pending: the wire keeps the Σ, .grad settles it when read
             self.k.unpack_sgd(self.tree, ALL, self.d_wire, self._div, self.d_theta, mom, lr,
                               momentum, nesterov, first, SLOT_INNER if write else -1)
-        self._synced = ((target[0], target[1], self._theta_versions()) if write else None)
+        self._synced = (target + (tver,)) if write else None
         return bufs
 
     def copy_to_inner(self, inner_params: Sequence[torch.Tensor]) -> None:
@@ -624,16 +703,17 @@ class DeviceOuterMirror:
         if self._delta is not None:  # the inner params are about to change: use them first
             self._take_delta()
             self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
-        self._relay_theta()
+        tver = self._relay_theta()
         s = self._synced
+        iptrs = _ptrs(inner)
         if (s is not None and len(s[0]) == len(inner)
                 and all(a is b for a, b in zip(s[0], inner))
-                and _sig(inner) == s[1] and self._theta_versions() == s[2]):
+                and iptrs == s[1] and _vers(inner) == s[2] and tver == s[3]):
             return
-        self.k.bind(self.tree, SLOT_INNER, inner, self.device)
+        self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))
         self.k.scatter(self.tree, ALL, self.d_theta, SLOT_INNER)
         if self.fused:
-            self._synced = (inner, _sig(inner), self._theta_versions())
+            self._synced = (inner, iptrs, _vers(inner), tver)
 
     def close(self) -> None:
         self.tree.close()

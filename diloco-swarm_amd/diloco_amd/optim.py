@@ -48,24 +48,37 @@ class OuterSGD(SGD):
                 "dampening=0, maximize=False")
         if g["nesterov"] and g["momentum"] == 0:
             raise ValueError("Nesterov momentum requires a momentum")
-        from .utils import device_path, has_mirror
-
-        if not has_mirror(self._model) and not device_path(g["params"][0]):
+        mirror = getattr(self._model, "_diloco_mirror", None)  # utils._ATTR
+        if mirror is None:
+            from .utils import device_path
+        if mirror is None and not device_path(g["params"][0]):
             # host tensors never stepped on the GPU (the reference's --device cpu runs):
             # torch.optim.SGD itself, as src/utils.py:62-63 builds it
             super().step()
             return loss
-        mirror = self._mirror()
+        if mirror is None:
+            mirror = self._mirror()
         params = g["params"]
         if len(params) != len(mirror.params) or any(a is not b for a, b in zip(params, mirror.params)):
             raise RuntimeError("OuterSGD parameters differ from its model's parameters()")
         momentum = float(g["momentum"])
-        host_bufs = [self.state[p].get("momentum_buffer") for p in params]
+        # self.state is keyed by tensor (a Python __hash__ per lookup): when it holds exactly
+        # the parameters in order -- every step after the first -- walk its values instead
+        st = self.state
+        same = len(st) == len(params) and all(k is p for k, p in zip(st.keys(), params))
+        if same:
+            host_bufs = [v.get("momentum_buffer") for v in st.values()]
+        else:
+            host_bufs = [st[p].get("momentum_buffer") for p in params]
         lr = g["lr"]
         if isinstance(lr, torch.Tensor):
             lr = float(lr.item())
         bufs = mirror.sgd_step(float(lr), momentum, bool(g["nesterov"]), host_bufs)
         if momentum != 0:
-            for p, b in zip(params, bufs):
-                self.state[p]["momentum_buffer"] = b
+            if same:
+                for v, b in zip(st.values(), bufs):
+                    v["momentum_buffer"] = b
+            else:
+                for p, b in zip(params, bufs):
+                    st[p]["momentum_buffer"] = b
         return loss

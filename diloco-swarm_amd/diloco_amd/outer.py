@@ -72,6 +72,26 @@ def pipelined_buckets(n_buckets: int, pack: Callable[[int], None],
         unpack(n_buckets - 1)
 
 
+U_BF16 = 2.0 ** -8   # unit roundoff of bf16 (8-bit significand, round to nearest even)
+U_F32 = 2.0 ** -24
+
+
+def bf16_codec_bound(sabs, n: int, exchange: str = "rccl"):
+    """The bf16 wire's error contract (config #5): per element, |g_bf16 - g_fp32| <= this, for
+    the averaged pseudo-gradient g of n peers, given sabs = Σ_r |d_r| over the peers' deltas
+    (numpy array or tensor). Each delta is rounded to bf16 (relative error <= u). exchange
+    "rccl" (the replicated bf16 all-reduce): n - 1 partial sums rounded to bf16 in whatever
+    order RCCL's ring adds them, each |S_k| <= (1+u)^n Σ|d_r|; "a2a" (the ordered exchange):
+    the bf16 slices summed in fp32 in rank order, never re-rounded. Then / n in fp32. First
+    order in u, plus the fp32 terms. The update θ_{s-1} - θ_s of Nesterov SGD carries
+    lr·((1+m)·bound_s + m²·bound_{s-1}) of it."""
+    if exchange == "a2a":
+        c = U_BF16 * (1.0 + n * U_F32) + (n + 1) * U_F32
+    else:
+        c = U_BF16 * (1.0 + (n - 1) * (1.0 + U_BF16) ** n) + (n + 1) * U_F32
+    return sabs * (c / n)
+
+
 class _Done:
     """Handle of a collective that completed synchronously (one replica, no process group)."""
 

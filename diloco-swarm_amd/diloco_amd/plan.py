@@ -84,12 +84,14 @@ class PackedTree:
             raise RuntimeError("PackedTree used after close()")
         return self._h
 
-    def bind(self, slot: int, tensors, stream) -> None:
+    def bind(self, slot: int, tensors, stream, key=None) -> None:
         """Upload the device addresses of `tensors` (fp32, contiguous) into `slot`.
 
-        No-op when the addresses are unchanged since the last bind of this slot.
+        No-op when the addresses are unchanged since the last bind of this slot. key: the
+        tuple of the tensors' addresses when the caller has it already.
         """
-        key = tuple([t.data_ptr() for t in tensors])
+        if key is None:
+            key = tuple([t.data_ptr() for t in tensors])
         if self._bound[slot] == key:  # fast path: same storage as last time (every outer step)
             return
         ptrs = []

@@ -47,7 +47,7 @@ import torch.nn as nn
 from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
-from .mirror import WRITE_BACKS, DeviceOuterMirror, HostOuterMirror, use_outer_parameters
+from .mirror import WRITE_BACKS, DeviceOuterMirror, HostOuterMirror, module_params
 from .optim import OuterSGD
 
 _ATTR = "_diloco_mirror"
@@ -137,9 +137,8 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     object.__setattr__(outer_model, _WRITE_BACK, write_back)
     object.__setattr__(outer_model, _FUSED, bool(fused) and placement == "device")
     if placement == "device":
-        if fused:
-            use_outer_parameters(outer_model)
-        outer_mirror(outer_model)  # lay the parameters out in the packed HBM arena now
+        # lay the parameters out in the packed HBM arena now (fused: as OuterParameters)
+        outer_mirror(outer_model)
     elif write_back == "deferred":
         # a checkpoint of the outer model waits for the write-back in flight
         outer_model.register_state_dict_pre_hook(lambda mod, prefix, keep_vars:
@@ -163,6 +162,10 @@ def _host_path(inner_model: nn.Module, outer_model: nn.Module) -> bool:
 
 def compute_pseudo_gradient(inner_model: nn.Module, outer_model: nn.Module) -> None:
     """outer.grad = outer - inner for every parameter (src/utils.py:218-221)."""
+    m = getattr(outer_model, _ATTR, None)
+    if m is not None:  # every call after the first: straight to the mirror
+        m.pseudo_gradient(module_params(inner_model))
+        return
     if _host_path(inner_model, outer_model):
         with torch.no_grad():
             for po, pi in zip(outer_model.parameters(), inner_model.parameters()):
@@ -170,11 +173,15 @@ def compute_pseudo_gradient(inner_model: nn.Module, outer_model: nn.Module) -> N
         return
     dev = _inner_device(inner_model)
     m = outer_mirror(outer_model, dev if dev.type != "cpu" else None)
-    m.pseudo_gradient(list(inner_model.parameters()))
+    m.pseudo_gradient(module_params(inner_model))
 
 
 def sync_inner_model(outer_model: nn.Module, inner_model: nn.Module) -> None:
     """inner = outer for every parameter (src/utils.py:223-226)."""
+    m = getattr(outer_model, _ATTR, None)
+    if m is not None:
+        m.copy_to_inner(module_params(inner_model))
+        return
     if _host_path(inner_model, outer_model):
         with torch.no_grad():
             for po, pi in zip(outer_model.parameters(), inner_model.parameters()):
@@ -182,7 +189,7 @@ def sync_inner_model(outer_model: nn.Module, inner_model: nn.Module) -> None:
         return
     dev = _inner_device(inner_model)
     m = outer_mirror(outer_model, dev if dev.type != "cpu" else None)
-    m.copy_to_inner(list(inner_model.parameters()))
+    m.copy_to_inner(module_params(inner_model))
 
 
 def get_optimizer(model: nn.Module, optimizer_config) -> Optimizer:

@@ -113,6 +113,9 @@ DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, 
 #define DL_TUNE_NT_LOADS 1
 #define DL_TUNE_NT_STORES 2
 #define DL_TUNE_WT_STORES 8 /* write-through (sc1) stores; tuning build only */
+/* two chunks per workgroup, both chunks' loads issued before the first store, in the
+ * 2-read / 1-write kernels (dl_delta_pack, dl_gather); no effect on the others */
+#define DL_TUNE_PAIRS 16
 #define DL_TUNE_AUTO (-1)
 DL_API int dl_tree_tune(dl_tree_t tree, int32_t max_blocks, int32_t flags);
 /* 1 in the tuning build (every load / store policy instantiated), 0 in the product library. */

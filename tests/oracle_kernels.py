@@ -61,7 +61,7 @@ class OracleKernels:
     def tree(self, numels, device, cap_elems=64 << 20, bucket_align=64):
         return CpuTree(numels, cap_elems, bucket_align)
 
-    def bind(self, tree, slot, tensors, device):
+    def bind(self, tree, slot, tensors, device, key=None):
         tree.slots[slot] = [t.detach().reshape(-1) for t in tensors]
 
     def _seg(self, tree, packed, i):

@@ -43,8 +43,8 @@ def test_header_constants_match_python_mirror():
     consts = dict(re.findall(r"#define (DL_\w+) \(?(-?\d+)\)?", src))
     assert int(consts["DL_TUNE_AUTO"]) == _lib.TUNE_AUTO
     assert (int(consts["DL_TUNE_NT_LOADS"]), int(consts["DL_TUNE_NT_STORES"]),
-            int(consts["DL_TUNE_WT_STORES"])) == (
-        _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_WT_STORES)
+            int(consts["DL_TUNE_WT_STORES"]), int(consts["DL_TUNE_PAIRS"])) == (
+        _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_WT_STORES, _lib.TUNE_PAIRS)
     assert "DL_TUNE_REVERSE" not in consts and "dl_tree_slot" not in src
     assert (int(consts["DL_COPY_WIDE"]), int(consts["DL_COPY_READ"]),
             int(consts["DL_COPY_WRITE"])) == (_lib.COPY_WIDE, _lib.COPY_READ, _lib.COPY_WRITE)

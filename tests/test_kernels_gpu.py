@@ -370,7 +370,8 @@ def test_store_policies_are_bit_identical(kernel, misaligned):
           "two_kernel": dict(fuse_single=False, tile_chunks=0, wire_dtype=wire)}[
               kernel.replace("_bf16", "")]
     NTL, NTS, WT = _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_WT_STORES
-    policies = [NTL, NTL | NTS]
+    PR = _lib.TUNE_PAIRS  # dl_delta_pack's two chunks per workgroup (odd counts, ragged)
+    policies = [NTL, NTL | NTS, NTL | PR, NTL | NTS | PR]
     if _lib.load().dl_tuning_build():
         policies += [NTL | WT, NTL | NTS | WT, WT, 0, NTS]
     ref_p = place()

@@ -266,3 +266,39 @@ def test_fused_outer_model_pickles_and_deepcopies_as_plain_parameters():
     sync_inner_model(outer, inner)
     assert _host(outer.parameters()).tobytes() == g["theta_s1"].tobytes()
     assert _host(inner.parameters()).tobytes() == g["theta_s1"].tobytes()
+
+
+def test_fused_outer_parameters_share_one_version_counter_and_flag_assignments():
+    """Fused: the outer parameters are OuterParameters made over views of the θ arena, so an
+    in-place write to any of them bumps the arena's one version counter; assigning .data or
+    .grad sets the mirror's flags, and the next call relays the new tensors into the arenas."""
+    from diloco_amd.mirror import OuterParameter
+
+    k = _Counting()
+    kernels.set_default_kernels(k)
+    inner, outer = _device_models(True)
+    m = outer._diloco_mirror
+    ps = list(outer.parameters())
+    assert all(isinstance(p, OuterParameter) for p in ps)
+    v0 = m.d_theta._version
+    with torch.no_grad():
+        ps[3].add_(1.0)
+    assert m.d_theta._version == v0 + 1
+    # .data assigned: relayed into the arena by the next call, inner gets it
+    new = torch.full_like(ps[2], 0.125)
+    ps[2].data = new
+    assert m.theta_touched
+    sync_inner_model(outer, inner)
+    assert ps[2].data_ptr() == m._ptrs["theta"][2]
+    assert torch.equal(list(inner.parameters())[2], new)
+    # .grad assigned by the user: the outer SGD steps on it (a stock-style outer step)
+    opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.5, momentum=0.0, nesterov=False))
+    g = [torch.full_like(p, 0.25) for p in ps]
+    before = [p.detach().clone() for p in ps]
+    for p, x in zip(ps, g):
+        p.grad = x
+    assert m.grads_touched
+    opt.step()
+    for p, b in zip(ps, before):
+        assert torch.equal(p.detach(), b - 0.5 * 0.25)
+        assert p.grad.data_ptr() != 0 and torch.equal(p.grad, torch.full_like(p, 0.25))

@@ -2,7 +2,8 @@
 """Launch the one-replica hot-path kernels cold, for rocprofv3 counter passes: each launch
 follows a 512 MiB default-policy dl_copy that evicts the Infinity Cache (bench.Scrubber), as
 the H inner steps of training do. Kernels: dl_delta_pack, dl_unpack_sgd (whole-range),
-dl_delta_sgd, dl_delta_pack_sgd, and dl_copy of T125's size with NT policy (the copy ceiling).
+dl_delta_sgd, dl_delta_pack_sgd, dl_delta_pack with two chunks per workgroup (DL_TUNE_PAIRS,
+k_walk_pairs in the trace), and dl_copy of T125's size with NT policy (the copy ceiling).
 
     python tools/cold_driver.py [tree] [reps]
 """
@@ -33,7 +34,11 @@ def main():
     two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
     one = OuterSync(params, world_size=1, fuse_single=True)
     kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True)
-    for e in (two, one, kept):
+    pairs = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
+    # AUTO's store policy for a whole-tree dl_delta_pack (NT above 2^28 elements), paired
+    big = pairs.tree.total >= (1 << 28)
+    pairs.tree.tune(0, _lib.TUNE_NT_LOADS | _lib.TUNE_PAIRS | (_lib.TUNE_NT_STORES if big else 0))
+    for e in (two, one, kept, pairs):
         e.step()  # steady-state SGD mode from here on
     n = spec.total() // 4 * 4
     a = torch.ones(n, device=dev)
@@ -44,7 +49,8 @@ def main():
         _lib.call("dl_copy", a.data_ptr(), b.data_ptr(), 4 * n, _lib.TUNE_NT_LOADS, st)
 
     for _ in range(reps):
-        for fn in (two.pseudo_gradient, two.apply, one.step, kept.step, copy):
+        for fn in (two.pseudo_gradient, two.apply, one.step, kept.step, pairs.pseudo_gradient,
+                   copy):
             scrub()
             fn()
     torch.cuda.synchronize()

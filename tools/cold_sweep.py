@@ -39,6 +39,42 @@ def timed_cold(fn, scrub):
     return e0.elapsed_time(e1)
 
 
+FLUSH_K = 3
+
+
+def _span(body):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    body()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def timed_flushed(fn, scrub, scrub_only_ms):
+    """--flushed: FLUSH_K (scrub, fn) cycles and a closing scrub as one span, minus
+    the same number of scrubs alone: fn charged with the HBM write-back of the lines it left
+    dirty in the Infinity Cache (which the plain cold timing's end event does not wait for)."""
+    scrub()
+
+    def body():
+        for _ in range(FLUSH_K):
+            scrub()
+            fn()
+        scrub()
+
+    return (_span(body) - scrub_only_ms) / FLUSH_K
+
+
+def scrub_only_span(scrub, reps=5):
+    def body():
+        for _ in range(FLUSH_K + 1):
+            scrub()
+
+    scrub()
+    return sorted(_span(body) for _ in range(reps))[reps // 2]
+
+
 def summarize(ms, nbytes):
     ms = sorted(ms)
     med = ms[len(ms) // 2]
@@ -54,8 +90,14 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--wire", default="f32", help="flags: the wire of the two-kernel and "
                     "kept-wire engines (f32 | bf16)")
+    ap.add_argument("--flushed", action="store_true",
+                    help="time each launch with its own dirty-line write-back (timed_flushed)")
     a = ap.parse_args()
     from bench import Scrubber
+
+    global timed_cold
+    if a.flushed:
+        plain = timed_cold  # noqa: F841 (kept for reference)
 
     dev = torch.device("cuda", 0)
     spec = get_tree(a.tree)
@@ -65,6 +107,10 @@ def main():
     synth.inner_tree_device([p.view(-1) for p in params], 1, 0, out=[p.view(-1) for p in params])
     scrub = Scrubber(dev)
     out = {"tree": a.tree, "params": P, "rounds": a.rounds}
+    if a.flushed:
+        base = scrub_only_span(scrub)
+        out["flushed"] = {"cycles": FLUSH_K, "scrub_only_ms": round(base, 4)}
+        timed_cold = lambda fn, scr: timed_flushed(fn, scr, base)  # noqa: E731
     what = a.what.split(",")
     if "flags" in what:
         wd = torch.bfloat16 if a.wire == "bf16" else torch.float32
@@ -88,10 +134,14 @@ def main():
                 "unpack_avg": (two, lambda: two.k.unpack_avg(two.tree, -1, scratch, 1, 0), 8)}
         half = (two.tree.n_chunks + 1) // 2
         # (flags, grid): grid half = two chunks per workgroup (grid-stride walk)
-        flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (0, 0): "plain",
-                      (2, 0): "nt_stores", (1, half): "nt_loads,2chunks/wg",
-                      (3, half): "nt_loads+stores,2chunks/wg", (_lib.TUNE_AUTO, 0): "auto",
-                      (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores"}
+        pr = _lib.TUNE_PAIRS
+        flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores",
+                      (1, half): "nt_loads,2chunks/wg", (3, half): "nt_loads+stores,2chunks/wg",
+                      (1 | pr, 0): "nt_loads,pairs", (3 | pr, 0): "nt_loads+stores,pairs",
+                      (_lib.TUNE_AUTO, 0): "auto"}
+        if _lib.load().dl_tuning_build():  # policies only the tuning build instantiates
+            flag_names.update({(0, 0): "plain", (2, 0): "nt_stores",
+                               (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores"})
         res = {(k, f): [] for k in kern for f in flag_names}
         for _ in range(a.rounds):
             for (k, f) in res:
@@ -157,8 +207,9 @@ def main():
                 "q8_reduce": (red, 2 * slot_bytes),
                 "unpack_sgd_q8": (unpack, slot_bytes + 20 * P)}
         shapes = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores", (1, half): "nt_loads,2chunks/wg",
-                  (3, half): "nt_loads+stores,2chunks/wg",
-                  (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores", (_lib.TUNE_AUTO, 0): "auto"}
+                  (3, half): "nt_loads+stores,2chunks/wg", (_lib.TUNE_AUTO, 0): "auto"}
+        if _lib.load().dl_tuning_build():  # AUTO already is write-through for the unpack
+            shapes[(1 | _lib.TUNE_WT_STORES, 0)] = "nt_loads+wt_stores"
         res = {(k, f): [] for k in kern for f in shapes}
         for _ in range(a.rounds):
             for (k, f) in res:

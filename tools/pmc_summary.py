@@ -20,6 +20,7 @@ def short(name):
     # most specific first: k_flat<UnpackSgd...> is dl_shard_sgd, UnpackSgdQ8 is not UnpackSgd
     names = {"k_xgmi_reduce_sgd": "xgmi_reduce_sgd", "k_flat": "shard_sgd", "DeltaQ8": "delta_q8", "UnpackSgdQ8": "unpack_sgd_q8",
              "k_q8_reduce": "q8_reduce", "DeltaPackSgd": "delta_pack_sgd",
+             "DeltaPackPair": "delta_pack_pairs", "GatherPair": "gather_pairs",
              "DeltaPack": "delta_pack", "UnpackSgd": "unpack_sgd",
              "UnpackAvg": "unpack_avg", "DeltaSgd": "delta_sgd", "Gather": "gather",
              "Scatter": "scatter", "k_fill_synth": "fill_synth",
