@@ -306,7 +306,8 @@ DL_API int dl_tree_tune(dl_tree_t t, int32_t max_blocks, int32_t flags) {
     return fail(DL_E_ARG, "dl_tree_tune: unknown flags 0x%x", flags);
 #ifndef DL_TUNING
   // the product build instantiates the AUTO policies only: NT loads, plain or NT stores
-  if (flags != DL_TUNE_AUTO && (!(flags & DL_TUNE_NT_LOADS) || (flags & DL_TUNE_WT_STORES)))
+  if (flags != DL_TUNE_AUTO &&
+      (!(flags & DL_TUNE_NT_LOADS) || (flags & (DL_TUNE_WT_STORES | DL_TUNE_PAIRS))))
     return fail(DL_E_ARG,
                 "dl_tree_tune: flags 0x%x need the tuning build (make TUNING=1): the product "
                 "library has NT loads with plain or NT stores only", flags);
@@ -399,11 +400,9 @@ constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // write-through only for the int8 unpack below 2^28 elements.
 constexpr int32_t kAutoWT = DL_TUNE_NT_LOADS | DL_TUNE_WT_STORES;
 enum class Big { keep, nt_stores, nt_stores_2 };
-// dl_delta_pack / dl_gather: two chunks per workgroup under AUTO (DL_TUNE_PAIRS)
-#ifndef DL_AUTO_PAIRS
-#define DL_AUTO_PAIRS 0
-#endif
-constexpr bool kAutoPairs = DL_AUTO_PAIRS != 0;
+// dl_delta_pack / dl_gather with two chunks per workgroup (DL_TUNE_PAIRS, tuning build only):
+// measured slower (dl_kernels.hip), so never part of AUTO
+constexpr bool kAutoPairs = false;
 
 int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char* who,
                 int32_t auto_flags = kAutoOther, Big big = Big::keep) {

@@ -184,7 +184,8 @@ hipError_t launch_walk(const Launch& L, const Body& body, int32_t grid) {
   return hipGetLastError();
 }
 
-// The pair walker: workgroup i takes chunks 2i and 2i+1 of the range (run2 issues both
+#ifdef DL_TUNING
+// The pair walker (tuning build): workgroup i takes chunks 2i and 2i+1 of the range (run2 issues both
 // chunks' loads before any store); a last odd chunk goes through run. Grid = ceil(n / 2), or
 // the tree's cap with a grid-stride over pairs.
 template <class Body, bool NTL, int NTS>
@@ -210,6 +211,8 @@ hipError_t launch_pairs(const Launch& L, const Body& body, int32_t grid) {
                      L.chunks, L.c0, L.c1, L.caddr, L.nchunk, body);
   return hipGetLastError();
 }
+
+#endif  // DL_TUNING
 
 // bodies whose AUTO policy stores write-through declare kWriteThrough = true
 template <class B, class = void>
@@ -243,6 +246,7 @@ hipError_t run(const Launch& L, const Body& body) {
   return launch_walk<Body, true, kStPlain>(L, body, grid);
 }
 
+#ifdef DL_TUNING
 // run() for a pair-capable body (DeltaPackPair, GatherPair): NT loads, plain / NT stores
 template <class Body>
 hipError_t run_pairs(const Launch& L, const Body& body) {
@@ -254,6 +258,7 @@ hipError_t run_pairs(const Launch& L, const Body& body) {
   if (L.flags & DL_TUNE_NT_STORES) return launch_pairs<Body, true, kStNT>(L, body, grid);
   return launch_pairs<Body, true, kStPlain>(L, body, grid);
 }
+#endif  // DL_TUNING
 
 }  // namespace
 }  // namespace dl

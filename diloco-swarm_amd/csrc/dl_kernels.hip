@@ -57,11 +57,14 @@ struct DeltaPack {
   }
 };
 
+#ifdef DL_TUNING
 // Two chunks per workgroup, every load of both issued before the first store: 8 float4 per
-// lane per input stream in flight instead of 4 (the 2-read / 1-write kernels are latency-bound
-// at 4: SQ_WAIT_ANY / SQ_WAVE_CYCLES 0.6 vs 0.3 for the SGD kernels). Used by
-// dl_delta_pack and dl_gather under DL_TUNE_AUTO (run_pairs). A misaligned tensor (the
-// scalar path) takes the one-chunk body for both chunks.
+// lane per input stream in flight instead of 4 (were the 2-read / 1-write
+// kernels latency-bound at 4?). Measured cold and interleaved (profiles/r03_pairs_ab.txt): 2-4 %
+// SLOWER than one chunk per workgroup for dl_delta_pack and dl_gather on T125 and T1.3B, with
+// SQ_WAIT_ANY up (0.61 -> 0.72) and the DRAM read-credit stalls unchanged (0.058): the reads
+// are limited by the memory controller, not by loads in flight. Tuning build only
+// (DL_TUNE_PAIRS). A misaligned tensor takes the one-chunk body for both chunks.
 template <typename W>
 struct DeltaPackPair {
   DeltaPack<W> one;
@@ -112,6 +115,8 @@ struct DeltaPackPair {
     if (i1 < k1.len) WireIO<W>::st1(w1, i1, th1[i1] - in1[i1]);
   }
 };
+
+#endif  // DL_TUNING
 
 // a3 unpack: dst = wire / d
 template <typename W, bool DIV>
@@ -380,6 +385,7 @@ struct Gather {
   }
 };
 
+#ifdef DL_TUNING
 template <typename W>
 struct GatherPair {
   Gather<W> one;
@@ -422,6 +428,8 @@ struct GatherPair {
     if (i1 < k1.len) WireIO<W>::st1(p1, i1, s1[i1]);
   }
 };
+
+#endif  // DL_TUNING
 
 // packed fp32 -> per-tensor fp32
 struct Scatter {
@@ -673,12 +681,18 @@ hipError_t launch_probe(bool write, int streams, const void* src, void* dst, int
 
 hipError_t launch_delta_pack(const Launch& L, int inner_slot, const float* outer, void* wire,
                              int wire_dtype) {
+#ifdef DL_TUNING
   if (wire_dtype == DL_BF16) {
     const DeltaPack<bf16_t> one{inner_slot, outer, static_cast<bf16_t*>(wire)};
     return L.pairs ? run_pairs(L, DeltaPackPair<bf16_t>{one}) : run(L, one);
   }
   const DeltaPack<float> one{inner_slot, outer, static_cast<float*>(wire)};
   return L.pairs ? run_pairs(L, DeltaPackPair<float>{one}) : run(L, one);
+#else
+  if (wire_dtype == DL_BF16)
+    return run(L, DeltaPack<bf16_t>{inner_slot, outer, static_cast<bf16_t*>(wire)});
+  return run(L, DeltaPack<float>{inner_slot, outer, static_cast<float*>(wire)});
+#endif
 }
 
 template <typename W>
@@ -907,12 +921,17 @@ hipError_t launch_delta_pack_sgd(const Launch& L, int inner_slot, float* outer, 
 }
 
 hipError_t launch_gather(const Launch& L, int src_slot, void* packed, int dtype) {
+#ifdef DL_TUNING
   if (dtype == DL_BF16) {
     const Gather<bf16_t> one{src_slot, static_cast<bf16_t*>(packed)};
     return L.pairs ? run_pairs(L, GatherPair<bf16_t>{one}) : run(L, one);
   }
   const Gather<float> one{src_slot, static_cast<float*>(packed)};
   return L.pairs ? run_pairs(L, GatherPair<float>{one}) : run(L, one);
+#else
+  if (dtype == DL_BF16) return run(L, Gather<bf16_t>{src_slot, static_cast<bf16_t*>(packed)});
+  return run(L, Gather<float>{src_slot, static_cast<float*>(packed)});
+#endif
 }
 
 hipError_t launch_scatter(const Launch& L, const float* packed, int dst_slot) {

@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import weakref
 from collections import OrderedDict
+from operator import is_
 from typing import List, Optional, Sequence
 
 import torch
@@ -310,14 +311,18 @@ _GRAD = torch._C.TensorBase.grad
 _DATA = torch._C.TensorBase.data
 
 
+_DATA_PTR = torch._C.TensorBase.data_ptr
+_VERSION = torch._C.TensorBase._version.__get__
+
+
 def _ptrs(ts: Sequence[torch.Tensor]) -> List[int]:
-    return [t.data_ptr() for t in ts]
+    return list(map(_DATA_PTR, ts))
 
 
 def _vers(ts: Sequence[torch.Tensor]) -> List[int]:
     """Version counters: any in-place torch write bumps them (kernel writes through the packed
     arenas and writes through `.data` do not)."""
-    return [t._version for t in ts]
+    return list(map(_VERSION, ts))
 
 
 def module_params(model: torch.nn.Module) -> List[torch.nn.Parameter]:
@@ -664,7 +669,7 @@ class DeviceOuterMirror:
             bufs = self._views["mom"]
             src = self._mom_src
             if not (src is not None and len(host_bufs) == len(src)
-                    and all(a is b for a, b in zip(host_bufs, src))):
+                    and all(map(is_, host_bufs, src))):
                 have = [b is not None for b in host_bufs]
                 if any(have) and not all(have):
                     raise RuntimeError("momentum buffers exist for some outer parameters only")
@@ -707,7 +712,7 @@ class DeviceOuterMirror:
         s = self._synced
         iptrs = _ptrs(inner)
         if (s is not None and len(s[0]) == len(inner)
-                and all(a is b for a, b in zip(s[0], inner))
+                and all(map(is_, s[0], inner))
                 and iptrs == s[1] and _vers(inner) == s[2] and tver == s[3]):
             return
         self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))

@@ -9,8 +9,12 @@ writes θ and the momentum buffers back to the host tensors the optimizer owns.
 """
 from __future__ import annotations
 
+from itertools import chain
+from operator import is_
+
 import torch
 from torch.optim import SGD
+from torch.optim import optimizer as _optim
 
 from .mirror import HostOuterMirror
 
@@ -33,8 +37,35 @@ class OuterSGD(SGD):
         flush_outer_model(self._model)
         return super().state_dict()
 
-    @torch.no_grad()
     def step(self, closure=None):
+        """torch.optim.Optimizer's step wrapper (profile_hook_step) restated: the pre / post
+        hooks (global and per-optimizer) run as there, but the record_function annotation is
+        made only while the autograd profiler runs -- it is a quarter of the host time of an
+        outer step otherwise (the kernel itself is one launch)."""
+        args, kwargs = (self,), ({} if closure is None else {"closure": closure})
+        for pre in chain(_optim._global_optimizer_pre_hooks.values(),
+                         self._optimizer_step_pre_hooks.values()):
+            res = pre(self, args, kwargs)
+            if res is not None:
+                if isinstance(res, tuple) and len(res) == 2:
+                    args, kwargs = res
+                else:
+                    raise RuntimeError(f"{self.step} must return None or a tuple of "
+                                       f"(new_args, new_kwargs), but got {res}.")
+        if torch.autograd._profiler_enabled():
+            with torch.autograd.profiler.record_function(f"Optimizer.step#{type(self).__name__}.step"):
+                out = self._step(*args[1:], **kwargs)
+        else:
+            out = self._step(*args[1:], **kwargs)
+        self._optimizer_step_code()
+        for post in chain(self._optimizer_step_post_hooks.values(),
+                          _optim._global_optimizer_post_hooks.values()):
+            post(self, args, kwargs)
+        return out
+
+    step.hooked = True  # torch.optim.Optimizer._patch_step_function: already wrapped (above)
+
+    def _step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -53,19 +84,20 @@ class OuterSGD(SGD):
             from .utils import device_path
         if mirror is None and not device_path(g["params"][0]):
             # host tensors never stepped on the GPU (the reference's --device cpu runs):
-            # torch.optim.SGD itself, as src/utils.py:62-63 builds it
-            super().step()
+            # torch.optim.SGD itself, as src/utils.py:62-63 builds it (its own no_grad)
+            fn = SGD.step  # hook-wrapped once a plain SGD exists: the hooks ran above
+            (fn.__wrapped__ if getattr(fn, "hooked", False) else fn)(self)
             return loss
         if mirror is None:
             mirror = self._mirror()
         params = g["params"]
-        if len(params) != len(mirror.params) or any(a is not b for a, b in zip(params, mirror.params)):
+        if len(params) != len(mirror.params) or not all(map(is_, params, mirror.params)):
             raise RuntimeError("OuterSGD parameters differ from its model's parameters()")
         momentum = float(g["momentum"])
         # self.state is keyed by tensor (a Python __hash__ per lookup): when it holds exactly
         # the parameters in order -- every step after the first -- walk its values instead
         st = self.state
-        same = len(st) == len(params) and all(k is p for k, p in zip(st.keys(), params))
+        same = len(st) == len(params) and all(map(is_, st.keys(), params))
         if same:
             host_bufs = [v.get("momentum_buffer") for v in st.values()]
         else:

@@ -106,15 +106,15 @@ DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, 
  * per-kernel choice -- NT loads everywhere; NT stores in the SGD kernels and, over launches of
  * more than 2^28 elements, in dl_delta_pack / dl_gather / dl_scatter / dl_unpack_avg;
  * write-through stores in dl_unpack_sgd_q8 below that size) or DL_TUNE_NT_LOADS [|
- * DL_TUNE_NT_STORES] for every kernel. Plain loads and DL_TUNE_WT_STORES (write-through, sc1)
- * for every kernel exist only in the tuning build (make TUNING=1, dl_tuning_build() == 1);
+ * DL_TUNE_NT_STORES] for every kernel. Plain loads, DL_TUNE_WT_STORES (write-through, sc1)
+ * for every kernel and DL_TUNE_PAIRS exist only in the tuning build (make TUNING=1, dl_tuning_build() == 1);
  * the product library rejects them with DL_E_ARG. Results are identical for every setting;
  * only speed differs. */
 #define DL_TUNE_NT_LOADS 1
 #define DL_TUNE_NT_STORES 2
 #define DL_TUNE_WT_STORES 8 /* write-through (sc1) stores; tuning build only */
-/* two chunks per workgroup, both chunks' loads issued before the first store, in the
- * 2-read / 1-write kernels (dl_delta_pack, dl_gather); no effect on the others */
+/* tuning build only: two chunks per workgroup, both chunks' loads issued before the first
+ * store, in the 2-read / 1-write kernels (dl_delta_pack, dl_gather; measured slower) */
 #define DL_TUNE_PAIRS 16
 #define DL_TUNE_AUTO (-1)
 DL_API int dl_tree_tune(dl_tree_t tree, int32_t max_blocks, int32_t flags);

@@ -371,13 +371,13 @@ def test_store_policies_are_bit_identical(kernel, misaligned):
               kernel.replace("_bf16", "")]
     NTL, NTS, WT = _lib.TUNE_NT_LOADS, _lib.TUNE_NT_STORES, _lib.TUNE_WT_STORES
     PR = _lib.TUNE_PAIRS  # dl_delta_pack's two chunks per workgroup (odd counts, ragged)
-    policies = [NTL, NTL | NTS, NTL | PR, NTL | NTS | PR]
+    policies = [NTL, NTL | NTS]
     if _lib.load().dl_tuning_build():
-        policies += [NTL | WT, NTL | NTS | WT, WT, 0, NTS]
+        policies += [NTL | WT, NTL | NTS | WT, WT, 0, NTS, NTL | PR, NTL | NTS | PR]
     ref_p = place()
     ref = OuterSync(ref_p, world_size=1, **kw)
     if not _lib.load().dl_tuning_build():
-        for f in (NTL | WT, WT, 0, NTS):
+        for f in (NTL | WT, WT, 0, NTS, NTL | PR):
             with pytest.raises(_lib.DilocoHipError, match="TUNING"):
                 ref.tree.tune(0, f)
     runs = []

@@ -34,11 +34,14 @@ def main():
     two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
     one = OuterSync(params, world_size=1, fuse_single=True)
     kept = OuterSync(params, world_size=1, fuse_single=True, keep_wire=True)
-    pairs = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
-    # AUTO's store policy for a whole-tree dl_delta_pack (NT above 2^28 elements), paired
-    big = pairs.tree.total >= (1 << 28)
-    pairs.tree.tune(0, _lib.TUNE_NT_LOADS | _lib.TUNE_PAIRS | (_lib.TUNE_NT_STORES if big else 0))
-    for e in (two, one, kept, pairs):
+    pairs = None
+    if _lib.load().dl_tuning_build():  # DL_TUNE_PAIRS exists in the tuning build only
+        pairs = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
+        # AUTO's store policy for a whole-tree dl_delta_pack (NT above 2^28 elements), paired
+        big = pairs.tree.total >= (1 << 28)
+        pairs.tree.tune(0, _lib.TUNE_NT_LOADS | _lib.TUNE_PAIRS
+                        | (_lib.TUNE_NT_STORES if big else 0))
+    for e in (two, one, kept) + ((pairs,) if pairs else ()):
         e.step()  # steady-state SGD mode from here on
     n = spec.total() // 4 * 4
     a = torch.ones(n, device=dev)
@@ -49,8 +52,10 @@ def main():
         _lib.call("dl_copy", a.data_ptr(), b.data_ptr(), 4 * n, _lib.TUNE_NT_LOADS, st)
 
     for _ in range(reps):
-        for fn in (two.pseudo_gradient, two.apply, one.step, kept.step, pairs.pseudo_gradient,
-                   copy):
+        for fn in (two.pseudo_gradient, two.apply, one.step, kept.step,
+                   pairs.pseudo_gradient if pairs else None, copy):
+            if fn is None:
+                continue
             scrub()
             fn()
     torch.cuda.synchronize()

@@ -137,11 +137,11 @@ def main():
         pr = _lib.TUNE_PAIRS
         flag_names = {(1, 0): "nt_loads", (3, 0): "nt_loads+stores",
                       (1, half): "nt_loads,2chunks/wg", (3, half): "nt_loads+stores,2chunks/wg",
-                      (1 | pr, 0): "nt_loads,pairs", (3 | pr, 0): "nt_loads+stores,pairs",
                       (_lib.TUNE_AUTO, 0): "auto"}
         if _lib.load().dl_tuning_build():  # policies only the tuning build instantiates
             flag_names.update({(0, 0): "plain", (2, 0): "nt_stores",
-                               (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores"})
+                               (1 | _lib.TUNE_WT_STORES, 0): "nt_loads+wt_stores",
+                               (1 | pr, 0): "nt_loads,pairs", (3 | pr, 0): "nt_loads+stores,pairs"})
         res = {(k, f): [] for k in kern for f in flag_names}
         for _ in range(a.rounds):
             for (k, f) in res:

@@ -2,6 +2,8 @@
 # bit-identity tests, then the cold A/B interleaved in one process (tools/cold_sweep.py flags)
 # on T125 and T1.3B, then the SQ wait / DRAM credit counters of both dl_delta_pack forms.
 R=$GRAFT_REPO_ROOT; cd $R && mkdir -p gpurun_out/pairs
+# the pair walker is in the tuning build only (make -C diloco-swarm_amd/csrc TUNING=1)
+export DILOCO_HIP_LIB=$R/diloco-swarm_amd/lib/libdiloco_hip_tuning.so
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 150 --timeout-method thread -k "store_policies or ragged or micro or slot_rebound" > gpurun_out/pairs/pytest.log 2>&1 || { echo pytest failed; tail -30 gpurun_out/pairs/pytest.log; exit 1; }
 tail -1 gpurun_out/pairs/pytest.log
 timeout -k 10 300 python tools/cold_sweep.py --tree t125 --rounds 11 --what flags --out gpurun_out/pairs/sweep_t125.json > gpurun_out/pairs/sweep_t125.txt 2>&1 || { echo sweep t125 failed; tail gpurun_out/pairs/sweep_t125.txt; exit 1; }

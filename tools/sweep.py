@@ -3,6 +3,10 @@
 process (cdna_hip_programming.md §5.4 rule 24). Prints median / min ms and GB/s per variant.
 
     python tools/sweep.py [--tree t125] [--rounds 15]
+
+Flags other than AUTO and NT loads [+ NT stores / DL_TUNE_PAIRS] exist only in the tuning
+build: make -C diloco-swarm_amd/csrc TUNING=1 and DILOCO_HIP_LIB=<repo>/diloco-swarm_amd/lib/
+libdiloco_hip_tuning.so (the product library rejects them).
 """
 import argparse
 import json

@@ -6,6 +6,10 @@ rotating order, median over rounds. Tile 0 = the whole-range launches (no blocki
 one-pass dl_delta_sgd is timed beside them as the floor.
 
     python tools/tile_ab.py [--tree t125] [--rounds 12] [--steps 10] [--out file.json]
+
+Flags other than AUTO and NT loads [+ NT stores / DL_TUNE_PAIRS] exist only in the tuning
+build: make -C diloco-swarm_amd/csrc TUNING=1 and DILOCO_HIP_LIB=<repo>/diloco-swarm_amd/lib/
+libdiloco_hip_tuning.so (the product library rejects them).
 """
 import argparse
 import json
