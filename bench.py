@@ -968,6 +968,76 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync",
     return res
 
 
+def run_dropin(spec, dev, ws, rank, steps, warmup):
+    """The outer step through the reference's own call surface, src/train.py:263-269 --
+    compute_pseudo_gradient -> TrainingComm.sync_gradients -> outer_optimizer.step() ->
+    sync_inner_model -- on the device-resident fused outer model (get_outer_model(...,
+    placement="device"), mirror.DeviceOuterMirror): K steps back to back between barrier +
+    synchronize, as the engine legs are timed (the four Python calls of step k+1 are issued
+    while step k's kernels run). N = 1: one dl_delta_pack_sgd per step; N > 1: per bucket
+    dl_delta_pack -> RCCL all_reduce, then dl_unpack_sgd (/n, SGD, inner write)."""
+    from types import SimpleNamespace
+
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+
+    if not dist.is_initialized():
+        import tempfile
+
+        dist.init_process_group("gloo", init_method="file://" + tempfile.mktemp(prefix="dlpg"),
+                                rank=0, world_size=1)
+    shapes = [s for _, s in spec.params()]
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList(
+        [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
+    outer = get_outer_model(inner, "device", fused=True)
+    opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
+    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    # inner = θ_0 + this rank's noise (H inner steps' stand-in); later steps see inner = θ
+    synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
+                            out=[p.data.view(-1) for p in inner.parameters()])
+
+    def one():
+        compute_pseudo_gradient(inner, outer)
+        comm.sync_gradients(outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+
+    for _ in range(max(warmup, 1)):
+        one()
+    _sync(ws)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(steps):
+        one()
+    ev[1].record()
+    _sync(ws)
+    dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
+    loop_ms = ev[0].elapsed_time(ev[1]) / steps
+    P = spec.total()
+    m = outer._diloco_mirror
+    res = {"tree": spec.name, "params": P, "tensors": len(shapes), "padded": m.tree.total,
+           "buckets": m.tree.n_buckets, "chunks": getattr(m.tree, "n_chunks", None),
+           "ms_per_step": dt * 1e3, "value": 4.0 * P / dt / 1e9,
+           "value_aggregate": ws * 4.0 * P / dt / 1e9, "loop_gpu_ms_per_step": round(loop_ms, 5),
+           "wire": "f32", "fused": m.fused,
+           "variant": ("the reference's four calls on the fused device outer model: "
+                       + ("dl_delta_pack_sgd" if ws == 1 else
+                          "dl_delta_pack -> RCCL all_reduce (per bucket) -> dl_unpack_sgd "
+                          "(/n, inner write)"))}
+    if ws == 1:
+        res["roofline"] = dict(kernel_entry(28 * P, loop_ms, load_pmc(spec.name).get("delta_pack_sgd"),
+                                            rw=(12 * P, 3, 16 * P, 4)),
+                               kernel="delta_pack_sgd", timing="timed loop GPU span / K")
+    m.close()
+    del outer, opt, inner, m
+    torch.cuda.empty_cache()
+    return res
+
+
 def dropin_overlap(spec, dev, ws, rank, cycles, inner_ms=50.0):
     """The host outer model in a training cycle: outer step, then `inner_ms` of GPU work
     standing in for the inner steps that follow (bf16 GEMMs; a T125 inner step of the
@@ -1599,6 +1669,8 @@ def main():
                 brief=False)
             leg(f"{spec.name}_dropin_device_eager", dropin_rate, spec, dev, ws, rank, 10,
                 "device", "sync", None, False, brief=False)
+            leg(f"{spec.name}_dropin_device_b2b", run_dropin, spec, dev, ws, rank, a.steps,
+                a.warmup, brief=False)
             leg(f"{spec.name}_dropin_overlap", dropin_overlap, spec, dev, ws, rank, 5,
                 brief=False)
         if ws == 1 and not a.no_cpu_baseline:
