@@ -6,11 +6,16 @@
         bench.py --gpus N --steps K --warmup W
 
 One step = one full outer step of src/train.py:261-269 over the whole synthetic tree on every
-rank, device-resident (θ_outer, momentum and the wire buffer live in HBM):
-    N = 1  dl_delta_pack (wire = θ_outer - inner) -> dl_unpack_sgd (Nesterov SGD, inner = θ)
-           (BASELINE config #2: the delta+pack kernels, no RCCL)
-    N > 1  dl_delta_pack -> RCCL reduce_scatter -> dl_shard_sgd (/n, SGD on this rank's 1/n)
-           -> RCCL all_gather(θ) -> dl_scatter to inner, bucketed and pipelined
+rank, device-resident (θ_outer, momentum and the wire buffer live in HBM), made through the
+reference's own calls -- compute_pseudo_gradient -> TrainingComm.sync_gradients ->
+outer_optimizer.step() -> sync_inner_model (diloco_amd's drop-in modules, src/train.py
+untouched) on the fused device outer model (get_outer_model(..., placement="device")):
+    N = 1  one dl_delta_pack_sgd (wire = outer.grad = θ_outer - inner, Nesterov SGD, inner = θ)
+           (BASELINE config #2's delta + pack, plus the SGD and copy-back the step needs)
+    N > 1  per bucket dl_delta_pack -> RCCL all_reduce, then dl_unpack_sgd (/n, SGD, inner = θ)
+The engine behind the fast path (OuterSync.step: N = 1 the same one-pass kernel; N > 1
+dl_delta_pack -> RCCL reduce_scatter -> dl_shard_sgd -> all_gather(θ) -> dl_scatter) is timed
+beside it ("extra.<tree>_engine", with its per-kernel, cold and back-to-back figures).
 Same tree per rank at every N (weak scaling). value = 4 * params / t_step (SURVEY.md §8d:
 "GB/s params reduced" = the bytes of ONE parameter tree reduced per DP step; max time over
 ranks); the weak-scaling aggregate N * 4 * params / t_step is reported beside it as
@@ -533,9 +538,17 @@ def rccl_reference(dev, ws, rank, elems, reps=5):
     (SUM) of `elems` elements, and a reduce_scatter + all_gather pair of the same size,
     back to back, max over ranks. busBW = 2(n-1)/n · bytes / t (the nccl-tests convention,
     SURVEY §8d): the measured 'algorithmic all-reduce bandwidth' the exchange is held to."""
+    out = {}
+    if dist.get_backend() == "gloo":
+        # a gloo rehearsal on one GPU (DILOCO_BENCH_BACKEND=gloo) stages whole tensors through
+        # host memory in every rank: 8 ranks x several copies of a 5 GB tree exceed the box's
+        # host-memory cap, and the rate would be gloo's anyway
+        cap = (256 << 20) // 4 // (64 * ws) * (64 * ws)
+        if elems > cap:
+            out["capped_for_gloo_elems"] = elems
+            elems = cap
     x = torch.ones(elems, device=dev)
     sh = torch.empty(elems // ws, device=dev)
-    out = {}
     for name in ("all_reduce", "reduce_scatter+all_gather"):
         for it in range(reps + 1):
             if it == 1:  # first call warms the communicator's buffers
@@ -1032,6 +1045,25 @@ def run_dropin(spec, dev, ws, rank, steps, warmup):
         res["roofline"] = dict(kernel_entry(28 * P, loop_ms, load_pmc(spec.name).get("delta_pack_sgd"),
                                             rw=(12 * P, 3, 16 * P, 4)),
                                kernel="delta_pack_sgd", timing="timed loop GPU span / K")
+    else:
+        # the exchange: the same all_reduce calls the step makes (every bucket of the packed
+        # .grad, on the DP group), back to back; bus bytes 2(n-1)/n of the fp32 wire
+        group = comm.dp.dp_group(dev)
+        reps_ar = max(3, steps // 2)
+        _sync(ws)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps_ar):
+            for lo, hi in m.tree.bucket_ranges:
+                dist.all_reduce(m.d_wire[lo:hi], group=group)
+        e1.record()
+        e1.synchronize()
+        ar_ms = _max_over_ranks(e0.elapsed_time(e1) / reps_ar, dev, ws)
+        bus = 2.0 * (ws - 1) / ws * 4 * m.tree.total
+        res["roofline"] = dict(kernel_entry(bus, ar_ms, bound="xgmi",
+                                            peak=(ws - 1) * XGMI_LINK_GBS),
+                               kernel="rccl all_reduce (all buckets, back to back)",
+                               bus_bytes_per_step=bus)
     m.close()
     del outer, opt, inner, m
     torch.cuda.empty_cache()
@@ -1491,18 +1523,36 @@ def main():
     # rocprofv3 averages describe the same launches; cache blocking is neutral on T125
     # (tools/tile_ab.py) and is what the T1.3B leg below runs (OuterSync's default tile)
     fallback = None
+    # The engine (OuterSync.step, the device-resident fast path): at N = 1 the one-replica step
+    # in one pass, pseudo-gradient kept (dl_delta_pack_sgd) -- with its per-kernel, cold and
+    # back-to-back figures; at N > 1 the sharded step.
     try:
-        # N = 1: the one-replica step in one pass, pseudo-gradient kept (dl_delta_pack_sgd)
-        main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap, fuse=ws == 1,
-                            b2b_loops=not a.no_b2b, tile=0, cold=not a.only_headline,
-                            keep_wire=True)
+        eng_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap, fuse=ws == 1,
+                           b2b_loops=not a.no_b2b, tile=0, cold=not a.only_headline,
+                           keep_wire=True)
     except Exception as e:  # N > 1: the replicated all-reduce step still gives the driver a line
         if ws == 1:
             raise
         fallback = repr(e)
-        log(f"sharded headline failed ({fallback}); measuring the all-reduce step instead")
-        main_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap, False,
-                            not a.no_b2b, False)
+        log(f"sharded engine step failed ({fallback}); measuring the all-reduce step instead")
+        eng_res = run_tree(spec, dev, ws, rank, a.steps, a.warmup, wire, cap, False,
+                           not a.no_b2b, False)
+    # The headline: the same outer step through the reference's own call surface
+    # (src/train.py:263-269 unchanged: compute_pseudo_gradient -> TrainingComm.sync_gradients
+    # -> outer_optimizer.step() -> sync_inner_model) on the fused device outer model; the
+    # engine's figure stays in extra. fp32 wire only (the drop-in surface has no wire knob).
+    main_res, dropin_error = eng_res, None
+    if wire == torch.float32:
+        try:
+            main_res = run_dropin(spec, dev, ws, rank, a.steps, a.warmup)
+            main_res["kernels"] = eng_res.get("kernels")
+            main_res["cold"] = eng_res.get("cold")
+            main_res["kernels_b2b"] = eng_res.get("kernels_b2b")
+        except Exception as e:
+            if ws == 1:
+                raise
+            dropin_error = repr(e)
+            log(f"drop-in headline failed ({dropin_error}); the engine's step is the headline")
     extra, parity = {}, {}
     ceiling = None
     if not a.only_headline:
@@ -1519,6 +1569,24 @@ def main():
         roof_cold = dict(with_copy_ceiling(ks[dom], ceiling), kernel=dom)
         cold = dict(cold, value=round(cold["value"], 3), warm_value=round(cold["warm_value"], 3),
                     kernels={k: with_copy_ceiling(v, ceiling) for k, v in ks.items()})
+    dropin = main_res is not eng_res
+    if dropin:
+        workload = (f"DiLoCo outer step, {spec.name} tree per rank, through the reference's "
+                    "calls (src/train.py:263-269: compute_pseudo_gradient -> "
+                    "TrainingComm.sync_gradients -> outer SGD step -> sync_inner_model) on the "
+                    "fused device-resident outer model: "
+                    + ("delta_pack -> RCCL all_reduce (per bucket) -> unpack_sgd (/n, Nesterov "
+                       "SGD, inner write)" if ws > 1 else
+                       "one dl_delta_pack_sgd per step (delta + outer.grad + Nesterov SGD + "
+                       "copy to inner; no exchange at one replica, src/comm.py:118-119)"))
+    else:
+        workload = (f"DiLoCo outer step, {spec.name} tree per rank: "
+                    + ("delta_pack -> RCCL reduce_scatter -> shard_sgd (1/n of θ, "
+                       "momentum) -> RCCL all_gather(θ) -> scatter to inner (bucketed, "
+                       "pipelined)" if ws > 1 else
+                       "delta + pack (wire = outer.grad) + Nesterov SGD + copy to inner "
+                       "in one pass (dl_delta_pack_sgd; no exchange at one replica, "
+                       "src/comm.py:118-119)"))
     em.line = {
         "metric": METRIC,
         "value": round(main_res["value"], 3),
@@ -1535,13 +1603,7 @@ def main():
         "dtype": "f32" if a.wire == "f32" else "f32 (bf16 wire)",
         "data": "synthetic (counter-based GPT-2-shaped tree, SURVEY.md §8d)",
         "config": {
-            "workload": (f"DiLoCo outer step, {spec.name} tree per rank: "
-                         + ("delta_pack -> RCCL reduce_scatter -> shard_sgd (1/n of θ, "
-                            "momentum) -> RCCL all_gather(θ) -> scatter to inner (bucketed, "
-                            "pipelined)" if ws > 1 else
-                            "delta + pack (wire = outer.grad) + Nesterov SGD + copy to inner "
-                            "in one pass (dl_delta_pack_sgd; no exchange at one replica, "
-                            "src/comm.py:118-119)")),
+            "workload": workload,
             "tree": spec.name, "params": main_res["params"], "tensors": main_res["tensors"],
             "wire": a.wire, "buckets": main_res["buckets"], "chunks": main_res["chunks"],
             "parallelism": f"dp{ws}",
@@ -1558,11 +1620,15 @@ def main():
         "extra": extra,
         "host": platform.node(),
     }
+    extra[f"{spec.name}_engine"] = _brief(eng_res) if dropin else None
+    if dropin_error:
+        em.line["headline_fallback"] = {"dropin_error": dropin_error}
     if fallback:
-        em.line["headline_fallback"] = {"variant": main_res["variant"], "sharded_error": fallback}
-        em.line["config"]["workload"] = (f"DiLoCo outer step, {spec.name} tree per rank: "
-                                         "delta_pack -> RCCL all_reduce -> unpack_sgd "
-                                         "(replicated; the sharded step failed)")
+        em.line["engine_fallback"] = {"variant": eng_res["variant"], "sharded_error": fallback}
+        if not dropin:
+            em.line["config"]["workload"] = (f"DiLoCo outer step, {spec.name} tree per rank: "
+                                             "delta_pack -> RCCL all_reduce -> unpack_sgd "
+                                             "(replicated; the sharded step failed)")
     log(f"headline done at {em.elapsed():.1f} s")
 
     def leg(name, fn, *args, into=extra, brief=True):
@@ -1669,8 +1735,6 @@ def main():
                 brief=False)
             leg(f"{spec.name}_dropin_device_eager", dropin_rate, spec, dev, ws, rank, 10,
                 "device", "sync", None, False, brief=False)
-            leg(f"{spec.name}_dropin_device_b2b", run_dropin, spec, dev, ws, rank, a.steps,
-                a.warmup, brief=False)
             leg(f"{spec.name}_dropin_overlap", dropin_overlap, spec, dev, ws, rank, 5,
                 brief=False)
         if ws == 1 and not a.no_cpu_baseline:
