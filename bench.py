@@ -1203,35 +1203,37 @@ def cpu_baseline(spec, seconds_budget=12.0):
     }
 
 
-def cpu_baseline_dist(spec, ws, rank, seconds_budget=12.0):
+def cpu_baseline_dist(spec, ws, rank, seconds_budget=12.0, group=None):
     """§8d CPU baseline at N > 1: this process is one of N fresh CPU processes (GPUs hidden)
     in a gloo group, each running the reference's per-tensor sequence on the full tree with
     one thread -- delta, per-tensor gloo all_reduce(SUM) + /= n, torch SGD-Nesterov, copy-back
     (oracle/torch_restatement.TorchOuterStep) -- N cores in all. Steps are counted so that the
     timed sample lasts about `seconds_budget`; value = 4P / t_step (the metric's definition),
-    max time over ranks."""
+    max time over ranks. group: a gloo group over the N ranks when the bench's own rank
+    processes run it (rehearsals with every rank on one GPU); default the child's world."""
     sys.path.insert(0, HERE)
     from oracle.torch_restatement import TorchOuterStep
 
+    group = group or dist.group.WORLD
     torch.set_num_threads(1)
     g = torch.Generator().manual_seed(rank)
     inner = [torch.empty(n).uniform_(-0.03, 0.03, generator=g) for n in spec.numels()]
-    st = TorchOuterStep(inner, group=dist.group.WORLD)
+    st = TorchOuterStep(inner, group=group)
     for t in inner:
         t.add_(torch.empty_like(t).uniform_(-1e-3, 1e-3, generator=g))
     st.step()  # creates the momentum buffers (not timed)
-    dist.barrier()
+    dist.barrier(group=group)
     t0 = time.perf_counter()
     st.step()
     one = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(one, op=dist.ReduceOp.MAX)
+    dist.all_reduce(one, op=dist.ReduceOp.MAX, group=group)
     k = max(2, int(seconds_budget / max(float(one.item()), 1e-3)))
-    dist.barrier()
+    dist.barrier(group=group)
     t0 = time.perf_counter()
     for _ in range(k):
         st.step()
     dt = torch.tensor([(time.perf_counter() - t0) / k], dtype=torch.float64)
-    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=group)
     t = float(dt.item())
     return {"value": round(4.0 * spec.total() / t / 1e9, 4), "unit": "GB/s", "cores": ws,
             "kind": "port",
@@ -1514,6 +1516,10 @@ def main():
     em = _Emitter(int(os.environ.get("RANK", "0")), a.deadline)
     soft = 0.7 * a.deadline
     ws, rank, dev = setup_dist(a.gpus)
+    # child legs put a second process per rank on the GPU: with every rank on one GPU (a gloo
+    # rehearsal) 2N + 1 processes (the launcher too) must stay within the box's 16 per GPU
+    shared_gpu = ws > max(1, torch.cuda.device_count())
+    children_fit = not shared_gpu or 2 * ws + 1 <= 16
     wire = torch.bfloat16 if a.wire == "bf16" else torch.float32
     cap = (a.bucket_mb << 20) // 4
     _lib.load()
@@ -1742,6 +1748,21 @@ def main():
             em.running = "cpu_baseline"
             log("timing the CPU baseline")
             em.line["cpu_baseline"] = cpu_baseline(spec)
+        elif ws > 1 and not a.no_cpu_baseline and not children_fit:
+            # every rank on one GPU (a gloo rehearsal): a child per rank would put 2N + 1
+            # processes on the card; the rank processes themselves run the N-core baseline
+            em.running = "cpu_baseline (in the rank processes)"
+            if a.deadline - _max_over_ranks(em.elapsed(), dev, ws) - 15 < 40:
+                em.skipped.append("cpu_baseline")
+            nthreads = torch.get_num_threads()
+            if "cpu_baseline" not in em.skipped:
+                r = _guard(cpu_baseline_dist, spec, ws, rank, 12.0,
+                           dist.new_group(backend="gloo"))
+                torch.set_num_threads(nthreads)
+                if isinstance(r, dict):
+                    r["ran_in"] = "the bench's rank processes (one GPU shared by all ranks)"
+                em.line["cpu_baseline"] = r
+                log(f"cpu_baseline done at {em.elapsed():.1f} s")
         elif ws > 1 and not a.no_cpu_baseline:
             # N CPU processes under gloo (one per rank, GPUs hidden): the reference's sequence
             # with its per-tensor all_reduce, N cores
@@ -1754,7 +1775,11 @@ def main():
                 em.line["cpu_baseline"] = isolated_legs(a, dev, ws, rank, min(150.0, left),
                                                         "cpu_baseline", HIDE_GPUS)
                 log(f"cpu_baseline done at {em.elapsed():.1f} s")
-        if ws > 1 and not a.no_xgmi:
+        if ws > 1 and not a.no_xgmi and not children_fit:
+            em.skipped += ["peer_access_legs (one GPU shared by all ranks: a child per rank "
+                           f"would put {2 * ws + 1} processes on it, the box allows 16)"] + [
+                f"rccl_env_{name}" for name in RCCL_ENV_VARIANTS]
+        elif ws > 1 and not a.no_xgmi:
             # last, in child processes: the direct peer-access exchange (IPC-mapped wires / θ,
             # one fused kernel), its parity check and the link probe
             left = a.deadline - _max_over_ranks(em.elapsed(), dev, ws) - 15
