@@ -981,14 +981,16 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync",
     return res
 
 
-def run_dropin(spec, dev, ws, rank, steps, warmup):
+def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32"):
     """The outer step through the reference's own call surface, src/train.py:263-269 --
     compute_pseudo_gradient -> TrainingComm.sync_gradients -> outer_optimizer.step() ->
     sync_inner_model -- on the device-resident fused outer model (get_outer_model(...,
     placement="device"), mirror.DeviceOuterMirror): K steps back to back between barrier +
     synchronize, as the engine legs are timed (the four Python calls of step k+1 are issued
     while step k's kernels run). N = 1: one dl_delta_pack_sgd per step; N > 1: per bucket
-    dl_delta_pack -> RCCL all_reduce, then dl_unpack_sgd (/n, SGD, inner write)."""
+    dl_delta_pack -> RCCL all_reduce, then dl_unpack_sgd (/n, SGD, inner write). wire="bf16":
+    BASELINE config #5 behind the same calls (the pack casts to bf16, RCCL sums bf16, the SGD
+    pass reads the wire)."""
     from types import SimpleNamespace
 
     from diloco_amd.comm import TrainingComm
@@ -1005,7 +1007,7 @@ def run_dropin(spec, dev, ws, rank, steps, warmup):
     inner = torch.nn.Module()
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
-    outer = get_outer_model(inner, "device", fused=True)
+    outer = get_outer_model(inner, "device", fused=True, wire=wire)
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     # inner = θ_0 + this rank's noise (H inner steps' stand-in); later steps see inner = θ
@@ -1036,7 +1038,7 @@ def run_dropin(spec, dev, ws, rank, steps, warmup):
            "buckets": m.tree.n_buckets, "chunks": getattr(m.tree, "n_chunks", None),
            "ms_per_step": dt * 1e3, "value": 4.0 * P / dt / 1e9,
            "value_aggregate": ws * 4.0 * P / dt / 1e9, "loop_gpu_ms_per_step": round(loop_ms, 5),
-           "wire": "f32", "fused": m.fused,
+           "wire": wire, "fused": m.fused,
            "variant": ("the reference's four calls on the fused device outer model: "
                        + ("dl_delta_pack_sgd" if ws == 1 else
                           "dl_delta_pack -> RCCL all_reduce (per bucket) -> dl_unpack_sgd "
@@ -1047,19 +1049,20 @@ def run_dropin(spec, dev, ws, rank, steps, warmup):
                                kernel="delta_pack_sgd", timing="timed loop GPU span / K")
     else:
         # the exchange: the same all_reduce calls the step makes (every bucket of the packed
-        # .grad, on the DP group), back to back; bus bytes 2(n-1)/n of the fp32 wire
+        # wire, on the DP group), back to back; bus bytes 2(n-1)/n of the wire
         group = comm.dp.dp_group(dev)
+        w = m.d_wire16 if wire == "bf16" else m.d_wire
         reps_ar = max(3, steps // 2)
         _sync(ws)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps_ar):
             for lo, hi in m.tree.bucket_ranges:
-                dist.all_reduce(m.d_wire[lo:hi], group=group)
+                dist.all_reduce(w[lo:hi], group=group)
         e1.record()
         e1.synchronize()
         ar_ms = _max_over_ranks(e0.elapsed_time(e1) / reps_ar, dev, ws)
-        bus = 2.0 * (ws - 1) / ws * 4 * m.tree.total
+        bus = 2.0 * (ws - 1) / ws * w.element_size() * m.tree.total
         res["roofline"] = dict(kernel_entry(bus, ar_ms, bound="xgmi",
                                             peak=(ws - 1) * XGMI_LINK_GBS),
                                kernel="rccl all_reduce (all buckets, back to back)",
@@ -1694,6 +1697,10 @@ def main():
                 if ws > 1:  # config #5 with the ordered exchange: bf16 slices summed in fp32
                     leg(f"{es.name}_bf16_a2a", run_tree, es, dev, ws, rank, ks, 1,
                         torch.bfloat16, cap, False, False, True, "a2a")
+                    # config #5 behind the reference's calls: the fused device outer model
+                    # with the bf16 wire (cast in the pack, SGD reading the wire)
+                    leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16",
+                        brief=False)
                     if not a.no_parity:  # both bf16 forms' error on this tree at this N
                         leg(f"bf16_codec_{es.name}", codec_error, es, dev, ws, rank, cap,
                             into=parity, brief=False)

@@ -176,16 +176,17 @@ class DPSync:
         num_peers = self.num_peers
         if num_peers == 1:
             return
-        params = list(model.parameters())
-        if not params:
-            return
-        from .utils import device_path, has_mirror, outer_mirror
-
-        if has_mirror(model):
+        m = getattr(model, "_diloco_mirror", None)  # utils._ATTR
+        if m is not None:
             # an outer model whose steps run on the GPU (host placement after a device
             # compute_pseudo_gradient, or placement="device"): its packed mirror reduces
-            m = outer_mirror(model)
             m.all_reduce(self.dp_group(m.device), num_peers)
+            return
+        from .mirror import module_params
+        from .utils import device_path
+
+        params = module_params(model)
+        if not params:
             return
         if not device_path(params[0]):
             # host tensors (the reference's --device cpu runs, or an outer model not yet

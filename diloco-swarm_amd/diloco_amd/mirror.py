@@ -40,7 +40,7 @@ import torch.distributed as dist
 from . import _lib
 from .kernels import default_kernels
 from .outer import pipelined_buckets
-from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER
+from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_GRAD, SLOT_INNER
 
 ALL = _lib.ALL_BUCKETS
 
@@ -55,6 +55,7 @@ def _check_host_params(params: Sequence[torch.Tensor]) -> None:
 
 
 WRITE_BACKS = ("sync", "deferred")
+OUTER_WIRES = ("f32", "bf16")
 
 
 class HostOuterMirror:
@@ -426,7 +427,10 @@ class DeviceOuterMirror:
     `.data` bypass version counters: call invalidate() after them)."""
 
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
-                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = False):
+                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = False,
+                 wire: str = "f32"):
+        if wire not in OUTER_WIRES:
+            raise ValueError(f"wire {wire!r}: one of {OUTER_WIRES}")
         self.params: List[torch.nn.Parameter] = module_params(outer_model)
         if not self.params:
             raise ValueError("outer model has no parameters")
@@ -445,6 +449,13 @@ class DeviceOuterMirror:
         self.d_theta = torch.zeros(self.tree.total, **z)
         self.d_wire = torch.zeros(self.tree.total, **z)
         self.d_mom: Optional[torch.Tensor] = None
+        # wire="bf16" (BASELINE config #5 behind the drop-in calls): at N > 1 the deltas cross
+        # the wire in bf16 (cast in the pack kernel, RCCL's bf16 SUM) and the SGD pass reads
+        # them from it; .grad shows the decoded average (the codec's value, not fp32's)
+        self.wire = wire
+        self.d_wire16 = (torch.zeros(self.tree.total, dtype=torch.bfloat16, device=self.device)
+                         if wire == "bf16" else None)
+        self._sum16 = False  # the pending Σ is in d_wire16 (.grad's arena is stale)
         # per-tensor views of each arena and their addresses, made once: the per-step checks
         # compare raw addresses (an outer step must not cost a Python tensor per parameter)
         self._views = {"theta": self._make_views(self.d_theta),
@@ -564,7 +575,7 @@ class DeviceOuterMirror:
     # ---- deferred work (fused mode) ------------------------------------------------------
     @property
     def pending(self) -> bool:
-        return self._delta is not None or self._div != 1
+        return self._delta is not None or self._div != 1 or self._sum16
 
     def _take_delta(self, tver_now=None) -> List[torch.Tensor]:
         """The pending delta's inner params, checked unchanged since compute_pseudo_gradient
@@ -588,7 +599,10 @@ class DeviceOuterMirror:
         if self._delta is not None:
             self._take_delta()
             self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
-        if self._div != 1:
+        if self._sum16:  # bf16 wire: the decoded average (/n in fp32) into .grad's arena
+            div, self._div, self._sum16 = self._div, 1, False
+            self.k.unpack_avg(self.tree, ALL, self.d_wire16, div, -1, self.d_wire)
+        elif self._div != 1:
             div, self._div = self._div, 1
             self.k.unpack_avg(self.tree, ALL, self.d_wire, div, -1, self.d_wire)
 
@@ -614,6 +628,7 @@ class DeviceOuterMirror:
         iptrs = _ptrs(inner)
         self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))
         self._div = 1  # the wire is overwritten: a /n still pending is moot
+        self._sum16 = False
         if self.fused:
             ivers = _vers(inner)
             self._delta = (inner, iptrs, ivers, tver)
@@ -624,6 +639,9 @@ class DeviceOuterMirror:
 
     def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
         """grad = Σ_peers grad / n (src/comm.py:120-123), in place on the packed .grad."""
+        if self.wire == "bf16":
+            self._all_reduce_bf16(group, num_peers)
+            return
         pack = None
         if self._delta is not None:  # fused: each bucket packed just before its collective
             self._take_delta()
@@ -649,6 +667,42 @@ class DeviceOuterMirror:
             (lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire)),
         )
         self._div = div
+
+    def _all_reduce_bf16(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
+        """The bf16 wire: per bucket, the deltas (a pending delta: dl_delta_pack straight to
+        bf16; else .grad's fp32 arena cast by dl_gather) -> RCCL all_reduce (bf16 SUM). Fused:
+        the Σ stays on the wire for the SGD pass (.grad decodes it when read); eager: decoded
+        into .grad with the /n at once (dl_unpack_avg)."""
+        w16 = self.d_wire16
+        if self._delta is not None:
+            self._take_delta()
+            self._relay_theta()
+            self._grad_views()
+
+            def pack(b):
+                self.k.delta_pack(self.tree, b, SLOT_INNER, self.d_theta, w16)
+        else:
+            if self.pending:
+                self.settle_grads()  # a second sync_gradients reduces the averages
+            self._relay_grads(zero_fill_missing=True)
+            self.k.bind(self.tree, SLOT_GRAD, self._views["wire"], self.device,
+                        key=tuple(self._ptrs["wire"]))
+
+            def pack(b):
+                self.k.gather(self.tree, b, SLOT_GRAD, w16)
+
+        def view(b):
+            lo, hi = self.tree.bucket_ranges[b]
+            return w16[lo:hi]
+
+        pipelined_buckets(
+            self.tree.n_buckets, pack,
+            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
+            (lambda b: None) if self.fused else
+            (lambda b: self.k.unpack_avg(self.tree, b, w16, num_peers, -1, self.d_wire)),
+        )
+        if self.fused:
+            self._div, self._sum16 = num_peers, True
 
     def sgd_step(self, lr: float, momentum: float, nesterov: bool,
                  host_bufs: Optional[List[Optional[torch.Tensor]]]) -> List[Optional[torch.Tensor]]:
@@ -695,8 +749,9 @@ class DeviceOuterMirror:
             if write:
                 self.k.bind(self.tree, SLOT_INNER, target[0], self.device, key=tuple(target[1]))
             # a pending /n stays pending: the wire keeps the Σ, .grad settles it when read
-            self.k.unpack_sgd(self.tree, ALL, self.d_wire, self._div, self.d_theta, mom, lr,
-                              momentum, nesterov, first, SLOT_INNER if write else -1)
+            self.k.unpack_sgd(self.tree, ALL, self.d_wire16 if self._sum16 else self.d_wire,
+                              self._div, self.d_theta, mom, lr, momentum, nesterov, first,
+                              SLOT_INNER if write else -1)
         self._synced = (target + (tver,)) if write else None
         return bufs
 

@@ -28,6 +28,10 @@ DILOCO_OUTER_PLACEMENT environment variable, "host" if unset):
             engine's kernel) and pack -> RCCL -> one SGD pass at N > 1; the parameters are
             mirror.OuterParameter, whose .grad completes the deferred work when read, and
             sync_inner_model is a verified no-op after the step (see DeviceOuterMirror).
+            wire (`get_outer_model(..., wire=)`, default from DILOCO_OUTER_WIRE, "f32"):
+            "bf16" sends the deltas over the DP exchange in bf16 (BASELINE config #5: the cast
+            in the pack kernel, the SGD fused into the unpack); .grad then shows the codec's
+            decoded average.
 
 Write-back of the host placement (`get_outer_model(..., write_back=)`, default from
 DILOCO_HOST_WRITEBACK, "sync" if unset): "sync" -- every call returns with the host tensors
@@ -47,7 +51,8 @@ import torch.nn as nn
 from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
-from .mirror import WRITE_BACKS, DeviceOuterMirror, HostOuterMirror, module_params
+from .mirror import (OUTER_WIRES, WRITE_BACKS, DeviceOuterMirror, HostOuterMirror,
+                     module_params)
 from .optim import OuterSGD
 
 _ATTR = "_diloco_mirror"
@@ -55,6 +60,7 @@ _OUTER = "_diloco_outer"
 _PLACEMENT = "_diloco_placement"
 _WRITE_BACK = "_diloco_write_back"
 _FUSED = "_diloco_fused"
+_WIRE = "_diloco_wire"
 PLACEMENTS = ("host", "device")
 
 
@@ -80,7 +86,8 @@ def outer_mirror(outer_model: nn.Module, device=None):
             if p is None:
                 raise ValueError("outer model has no parameters")
             m = DeviceOuterMirror(outer_model, p.device, kernels=k,
-                                  fused=getattr(outer_model, _FUSED, False))
+                                  fused=getattr(outer_model, _FUSED, False),
+                                  wire=getattr(outer_model, _WIRE, "f32"))
             object.__setattr__(outer_model, _ATTR, m)
             return m
         if device is None:
@@ -103,12 +110,13 @@ def _inner_device(inner_model: nn.Module) -> torch.device:
 
 
 def get_outer_model(inner_model: nn.Module, placement: str = None,
-                    write_back: str = None, fused: bool = None) -> nn.Module:
+                    write_back: str = None, fused: bool = None, wire: str = None) -> nn.Module:
     """Initializes the outer model from the inner model (src/utils.py:213-216).
 
     placement "host" (the reference's, default) or "device"; write_back "sync" (default) or
-    "deferred" for the host placement; fused (default on) for the device placement (see the
-    module docstring)."""
+    "deferred" for the host placement; fused (default on) and wire ("f32" default, "bf16":
+    BASELINE config #5's codec on the DP exchange) for the device placement (see the module
+    docstring)."""
     if placement is None:
         placement = os.environ.get("DILOCO_OUTER_PLACEMENT", "host")
     if placement not in PLACEMENTS:
@@ -119,6 +127,13 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
         raise ValueError(f"write_back {write_back!r}: one of {WRITE_BACKS}")
     if fused is None:
         fused = os.environ.get("DILOCO_OUTER_FUSED", "1") not in ("0", "")
+    if wire is None:
+        wire = os.environ.get("DILOCO_OUTER_WIRE", "f32")
+    if wire not in OUTER_WIRES:
+        raise ValueError(f"wire {wire!r}: one of {OUTER_WIRES}")
+    if wire != "f32" and placement != "device":
+        raise ValueError("the bf16 outer wire needs placement='device' (the host placement "
+                         "keeps the reference's fp32 host tensors end to end)")
     outer_model = copy.deepcopy(inner_model)
     if placement == "host":
         outer_model = outer_model.to("cpu")
@@ -136,6 +151,7 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     object.__setattr__(outer_model, _PLACEMENT, placement)
     object.__setattr__(outer_model, _WRITE_BACK, write_back)
     object.__setattr__(outer_model, _FUSED, bool(fused) and placement == "device")
+    object.__setattr__(outer_model, _WIRE, wire)
     if placement == "device":
         # lay the parameters out in the packed HBM arena now (fused: as OuterParameters)
         outer_mirror(outer_model)

@@ -47,3 +47,34 @@ def expected_rank_order(n, steps=2, wire="f32"):
         out[f"theta_s{s}"] = np.concatenate(st.theta)
         out[f"buf_s{s}"] = np.concatenate(st.buf)
     return out
+
+
+def expected_bf16_allreduce(n, steps=2):
+    """The outer step with a bf16 wire summed by the transport in bf16 (RCCL's / gloo's bf16
+    SUM: each replica's delta rounded to bf16, every partial sum rounded to bf16, in rank order)
+    and averaged in fp32 -- what the fused device outer model with wire="bf16" computes; the
+    order of the partial sums does not matter at n = 2. Micro tree; returns θ, the momentum
+    and the decoded average g (what .grad shows) per step."""
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from oracle import oracle
+
+    spec = get_tree("micro")
+    theta = [t.copy() for t in synth.outer_tree(spec.numels(), spec.init_spec())]
+    buf = [np.empty_like(t) for t in theta]
+    out = {}
+    for s in range(1, steps + 1):
+        inners = [synth.inner_tree(theta, s, r) for r in range(n)]
+        avg = []
+        for t in range(len(theta)):
+            d = [oracle.bf16_round(oracle.delta(theta[t], inners[r][t])) for r in range(n)]
+            acc = d[0]
+            for dr in d[1:]:
+                acc = oracle.bf16_round((acc + dr).astype(np.float32))
+            g = (acc / np.float32(n)).astype(np.float32)
+            oracle.sgd(theta[t], buf[t], g, 0.7, 0.9, True, s == 1)
+            avg.append(g)
+        out[f"theta_s{s}"] = np.concatenate(theta)
+        out[f"buf_s{s}"] = np.concatenate(buf)
+        out[f"avg_s{s}"] = np.concatenate(avg)
+    return out

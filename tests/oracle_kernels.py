@@ -68,17 +68,33 @@ class OracleKernels:
         o = int(tree.seg_off[i])
         return _np(packed)[o:o + tree.numels[i]]
 
+    def _rd(self, tree, packed, i):
+        """Segment i of a packed fp32 or bf16 buffer, as a fresh fp32 array."""
+        if packed.dtype == torch.bfloat16:
+            o = int(tree.seg_off[i])
+            return packed[o:o + tree.numels[i]].float().numpy().copy()
+        return self._seg(tree, packed, i).copy()
+
+    def _wr(self, tree, packed, i, x):
+        """Store fp32 values into segment i (a bf16 buffer: rounded to nearest even, as the
+        kernels' v_cvt_pk_bf16_f32; oracle.bf16_round, exact in bf16 afterwards)."""
+        if packed.dtype == torch.bfloat16:
+            o = int(tree.seg_off[i])
+            packed[o:o + tree.numels[i]] = torch.from_numpy(
+                oracle.bf16_round(np.ascontiguousarray(x, dtype=np.float32))).to(torch.bfloat16)
+        else:
+            self._seg(tree, packed, i)[:] = x
+
     def delta_pack(self, tree, bucket, inner_slot, theta, wire):
-        assert wire.dtype == torch.float32
         for i in tree.segs(bucket):
             d = oracle.delta(np.ascontiguousarray(self._seg(tree, theta, i)),
                              _np(tree.slots[inner_slot][i]).copy())
-            self._seg(tree, wire, i)[:] = d
+            self._wr(tree, wire, i, d)
 
     def unpack_sgd(self, tree, bucket, wire, divisor, theta, mom, lr, momentum, nesterov, first,
                    inner_slot):
         for i in tree.segs(bucket):
-            g = self._seg(tree, wire, i).copy()
+            g = self._rd(tree, wire, i)
             if divisor != 1:
                 g = (g / np.float32(divisor)).astype(np.float32)
             th = self._seg(tree, theta, i).copy()
@@ -186,7 +202,7 @@ class OracleKernels:
 
     def unpack_avg(self, tree, bucket, wire, divisor, dst_slot, dst_packed=None):
         for i in tree.segs(bucket):
-            g = self._seg(tree, wire, i).copy()
+            g = self._rd(tree, wire, i)
             if divisor != 1:
                 g = (g / np.float32(divisor)).astype(np.float32)
             if dst_slot >= 0:
@@ -196,7 +212,7 @@ class OracleKernels:
 
     def gather(self, tree, bucket, src_slot, packed):
         for i in tree.segs(bucket):
-            self._seg(tree, packed, i)[:] = _np(tree.slots[src_slot][i])
+            self._wr(tree, packed, i, _np(tree.slots[src_slot][i]))
 
     def scatter(self, tree, bucket, packed, dst_slot):
         for i in tree.segs(bucket):

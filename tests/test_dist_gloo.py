@@ -19,7 +19,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import PKG, REPO, load_npz, normwise_ok, split
-from expect import MICRO_Q8_CAP, expected_q8, expected_rank_order
+from expect import MICRO_Q8_CAP, expected_bf16_allreduce, expected_q8, expected_rank_order
 
 MICRO_STEPS = 2
 # stand-in for src/metrics.py Outputs (a pydantic model there); module level so it pickles
@@ -72,18 +72,20 @@ def _worker(rank, world, port, mode, num_stages, out):
     theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
     rec = {}
     if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_host",
-                "dropin_device_quiet", "dropin_device_eager"):
+                "dropin_device_quiet", "dropin_device_eager", "dropin_device_bf16",
+                "dropin_device_bf16_eager"):
         from diloco_amd.utils import flush_outer_model, has_mirror
 
         deferred = mode == "dropin_deferred"
         # quiet: nothing reads the outer model between the four calls (src/train.py:261-269),
         # so the fused device model defers the delta and the /n into its one SGD pass
-        quiet = mode == "dropin_device_quiet"
+        quiet = mode in ("dropin_device_quiet", "dropin_device_bf16")
         device = mode.startswith("dropin_device")
         inner = _micro_module(theta0, shapes)
         outer = get_outer_model(inner, placement="device" if device else None,
                                 write_back="deferred" if deferred else None,
-                                fused=mode != "dropin_device_eager")
+                                fused=not mode.endswith("_eager"),
+                                wire="bf16" if "bf16" in mode else None)
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
         assert type(opt).__name__ == "OuterSGD"
         from diloco_amd.utils import outer_mirror
@@ -93,7 +95,7 @@ def _worker(rank, world, port, mode, num_stages, out):
             assert type(outer_mirror(outer)).__name__ == (
                 "DeviceOuterMirror" if device else "HostOuterMirror")
             if device:
-                assert outer_mirror(outer).fused == (mode != "dropin_device_eager")
+                assert outer_mirror(outer).fused == (not mode.endswith("_eager"))
         comm = TrainingComm(world_, (1, 1, 32), None)
         for s in range(1, MICRO_STEPS + 1):
             prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
@@ -440,3 +442,19 @@ def test_gradsync_a2a_is_bit_exact_against_rank_order_oracle(world):
     if world == 4:  # the same through TrainingComm.sync_gradients (DILOCO_DP_EXCHANGE=a2a)
         for rec in _run("dpsync_a2a", world):
             assert rec["got"].tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("mode", ["dropin_device_bf16", "dropin_device_bf16_eager"])
+def test_dropin_device_bf16_wire_two_peers(mode):
+    """BASELINE config #5 behind the reference's calls (get_outer_model(..., wire="bf16")): the
+    deltas cross the DP exchange in bf16 and the SGD reads them from the wire. Two peers,
+    2 outer steps, fused (nothing read between the calls) and eager: θ, momentum, the inner
+    params and .grad (the codec's decoded average) bit-exact against the restatement of the
+    codec (tests/expect.expected_bf16_allreduce), every replica identical."""
+    exp = expected_bf16_allreduce(2)
+    recs = _run(mode, 2)
+    for rec in recs:
+        for s in (1, 2):
+            for k in ("theta", "buf", "avg"):
+                assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (mode, k, s)
+            assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), (mode, s)

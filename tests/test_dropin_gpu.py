@@ -50,7 +50,7 @@ def _flat(ts):
 
 
 def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=None,
-                 write_back=None, quiet=False, fused=None):
+                 write_back=None, quiet=False, fused=None, wire=None):
     """The reference's outer step sequence with the drop-in functions (this process = DP
     rank `rank` of `n`; the default process group must exist). quiet: nothing is read between
     the four calls (src/train.py:261-269 reads nothing), so a fused device outer model defers
@@ -66,7 +66,7 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
     shapes = [s for _, s in spec.params()]
     inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cpu")
     # src/train.py:382: before the inner model moves
-    outer = get_outer_model(inner, placement, write_back=write_back, fused=fused)
+    outer = get_outer_model(inner, placement, write_back=write_back, fused=fused, wire=wire)
     deferred = write_back == "deferred"
     inner = inner.to("cuda:0")
     if placement == "device":
@@ -194,11 +194,13 @@ def _worker(rank, world, port, mode, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     rec = {}
-    if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_device_quiet"):
+    if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_device_quiet",
+                "dropin_device_bf16"):
         rec = _outer_steps(rank, world,
                            placement="device" if mode.startswith("dropin_device") else None,
                            write_back="deferred" if mode == "dropin_deferred" else None,
-                           quiet=mode == "dropin_device_quiet")
+                           quiet=mode in ("dropin_device_quiet", "dropin_device_bf16"),
+                           wire="bf16" if mode == "dropin_device_bf16" else None)
     elif mode in ("engine", "engine_ar"):
         from diloco_amd import synth
         from diloco_amd.outer import OuterSync
@@ -320,6 +322,21 @@ def test_two_peers_on_gpu_match_reference(mode):
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
             if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
+
+
+def test_two_peers_on_gpu_bf16_outer_wire():
+    """Config #5's bf16 wire behind the reference's calls on the GPU (two processes, gloo DP
+    group on device tensors): the HIP pack casts to bf16, the SGD pass reads the wire; θ,
+    momentum, inner and .grad (decoded average) bit-exact against the codec's restatement."""
+    from expect import expected_bf16_allreduce
+
+    exp = expected_bf16_allreduce(2)
+    for rec in _run("dropin_device_bf16"):
+        for s in (1, 2):
+            assert rec[f"theta_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), s
+            assert rec[f"buf_s{s}"].tobytes() == exp[f"buf_s{s}"].tobytes(), s
+            assert rec[f"avg_s{s}"].tobytes() == exp[f"avg_s{s}"].tobytes(), s
+            assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), s
 
 
 @pytest.mark.parametrize("exchange", ["xgmi", "xgmi_inner"])

@@ -223,6 +223,39 @@ def main():
             print(f"{k:14s} {shapes[f]:26s} med {s['med_ms']:.4f} ms {s['med_GBs']:7.1f} GB/s"
                   f"  best {s['best_GBs']:7.1f}", flush=True)
         e.close()
+    if "pipe" in what:
+        # a producer and its consumer (VERDICT/ADVICE r02: are plain stores worth it when the
+        # next kernel re-reads the output?): the two-kernel step, whole range -- dl_delta_pack
+        # then dl_unpack_sgd -- under AUTO (plain wire stores below 2^28 elements) against every
+        # kernel's stores NT; and the DP grad sync's pack + average-back (dl_gather ->
+        # dl_unpack_avg, the all-reduce of one replica being the identity)
+        two = OuterSync(params, world_size=1, fuse_single=False, tile_chunks=0)
+        two.step()
+        scratch = torch.empty_like(two.theta)
+
+        def step2():
+            two.pseudo_gradient()
+            two.apply()
+
+        def sync2():
+            two.k.gather(two.tree, -1, 0, scratch)
+            two.k.unpack_avg(two.tree, -1, scratch, 1, 0)
+
+        kern = {"delta_pack+unpack_sgd": (step2, 36), "gather+unpack_avg": (sync2, 16)}
+        pol = {_lib.TUNE_AUTO: "auto", 3: "nt_loads+stores", 1: "nt_loads"}
+        res = {(k, f): [] for k in kern for f in pol}
+        for _ in range(a.rounds):
+            for (k, f) in res:
+                two.tree.tune(0, f)
+                res[(k, f)].append(timed_cold(kern[k][0], scrub))
+        two.tree.tune(0, _lib.TUNE_AUTO)
+        out["pipe"] = {}
+        for (k, f), ms in res.items():
+            st = summarize(ms, kern[k][1] * P)
+            out["pipe"].setdefault(k, {})[pol[f]] = st
+            print(f"{k:22s} {pol[f]:18s} med {st['med_ms']:.4f} ms {st['med_GBs']:7.1f} GB/s"
+                  f"  best {st['best_GBs']:7.1f}", flush=True)
+        two.close()
     if "tiles" in what:
         engs = {}
         for tile in (0, 1024, 2048, 4096, 8192, 16384):
