@@ -389,17 +389,16 @@ constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // is 2-8 % slower (tools/cold_sweep.py "auto", profiles/r02_cold_sweep_flags_auto_*.json).
 constexpr int32_t kBigLaunchChunks = (1 << 28) / DL_CHUNK_ELEMS;
 constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
-// Write-through (sc1) stores: cold, on T125-size launches, 0.5-4.0 % faster than the NT /
-// plain policy in 13 of 14 fp32 kernel-box pairs and 2.2-5.6 % for dl_unpack_sgd_q8 on three
-// boxes; 0.3-3.0 % slower over a whole T1.3B tree (tools/cold_sweep.py,
-// profiles/r02_cold_sweep_wt_*.json, r02_cold_sweep_q8_*.json). But a line stored
-// write-through is not there for the next step to re-read: with the SGD kernels write-through
-// the back-to-back (warm) T125 step fell from ~0.59 to 0.63 ms and the bench line to 785 GB/s
-// while the cold step gained ~1 % (profiles/r02_bench_n1_wt_auto.json,
-// r02_cold_sweep_autowt_*.json). So AUTO keeps NT / plain stores for the fp32 kernels and uses
-// write-through only for the int8 unpack below 2^28 elements.
-constexpr int32_t kAutoWT = DL_TUNE_NT_LOADS | DL_TUNE_WT_STORES;
-enum class Big { keep, nt_stores, nt_stores_2 };
+// Kernels whose output no kernel re-reads next (dl_scatter: the inner params; dl_unpack_avg:
+// gradients; dl_unpack_sgd_q8: θ, momentum, inner) store non-temporally at every size. Round 2
+// chose plain stores below 2^28 elements for the first two and write-through (sc1) for the int8
+// unpack from a cold timing whose end event did not wait for the lines a launch leaves dirty in
+// the Infinity Cache. Charged with that write-back (tools/cold_sweep.py --flushed,
+// profiles/r03_cold_sweep_flushed_t125.json): NT stores are 8 % faster than plain for dl_scatter
+// and dl_unpack_avg and 2.5 % faster than write-through for dl_unpack_sgd_q8 on T125-size
+// launches, equal over a whole T1.3B tree. The product library has no write-through stores.
+constexpr int32_t kAutoNT = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
+enum class Big { keep, nt_stores, nt_stores_2, two_chunks };
 // dl_delta_pack / dl_gather with two chunks per workgroup (DL_TUNE_PAIRS, tuning build only):
 // measured slower (dl_kernels.hip), so never part of AUTO
 constexpr bool kAutoPairs = false;
@@ -424,8 +423,9 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
   L->flags = t->flags == DL_TUNE_AUTO ? auto_flags : t->flags;
   L->pairs = (L->flags & DL_TUNE_PAIRS) != 0;
   if (t->flags == DL_TUNE_AUTO && big != Big::keep && L->c1 - L->c0 >= kBigLaunchChunks) {
-    L->flags = (L->flags & ~DL_TUNE_WT_STORES) | DL_TUNE_NT_STORES;  // WT -> NT above 2^28
-    if (big == Big::nt_stores_2 && L->grid == 0) L->grid = (L->c1 - L->c0 + 1) / 2;
+    L->flags |= DL_TUNE_NT_STORES;
+    if ((big == Big::nt_stores_2 || big == Big::two_chunks) && L->grid == 0)
+      L->grid = (L->c1 - L->c0 + 1) / 2;
   }
   L->stream = static_cast<hipStream_t>(s);
   return DL_OK;
@@ -476,7 +476,7 @@ DL_API int dl_delta_pack(dl_tree_t t, int32_t b, int32_t inner_slot, const float
 DL_API int dl_unpack_avg(dl_tree_t t, int32_t b, const void* wire, int32_t wire_dtype,
                          int32_t divisor, int32_t dst_slot, float* dst_packed, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_avg", kAutoOther, Big::nt_stores_2));
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_avg", kAutoNT, Big::two_chunks));
   DL_TRY(check_packed(wire, "dl_unpack_avg", "wire"));
   DL_TRY(check_dtype(wire_dtype, "dl_unpack_avg"));
   if (divisor < 1) return fail(DL_E_ARG, "dl_unpack_avg: divisor %d", divisor);
@@ -822,7 +822,7 @@ DL_API int dl_unpack_sgd_q8(dl_tree_t t, int32_t b, const void* slots, float* ou
                             float lr, float momentum, int32_t nesterov, int32_t first_step,
                             int32_t inner_slot, dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd_q8", kAutoWT, Big::nt_stores));
+  DL_TRY(make_launch(t, b, s, &L, "dl_unpack_sgd_q8", kAutoNT));
   DL_TRY(check_packed(slots, "dl_unpack_sgd_q8", "slots"));
   DL_TRY(check_packed(outer, "dl_unpack_sgd_q8", "outer"));
   if (momentum != 0.f) DL_TRY(check_packed(mom, "dl_unpack_sgd_q8", "momentum"));
@@ -853,7 +853,7 @@ DL_API int dl_gather(dl_tree_t t, int32_t b, int32_t src_slot, void* packed, int
 DL_API int dl_scatter(dl_tree_t t, int32_t b, const float* packed, int32_t dst_slot,
                       dl_stream_t s) {
   dl::Launch L;
-  DL_TRY(make_launch(t, b, s, &L, "dl_scatter", kAutoOther, Big::nt_stores_2));
+  DL_TRY(make_launch(t, b, s, &L, "dl_scatter", kAutoNT, Big::two_chunks));
   DL_TRY(check_slot(t, dst_slot, "dl_scatter"));
   DL_TRY(check_packed(packed, "dl_scatter", "packed"));
   DL_TRY(slot_begin(t, dst_slot, L.stream, "dl_scatter"));

@@ -150,8 +150,7 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 
 // ---- the walker ----------------------------------------------------------------------------
 // Body::run is instantiated per (NTL, NTS) policy. The product build instantiates what
-// DL_TUNE_AUTO selects: non-temporal loads with plain or non-temporal stores, and write-through
-// stores for the bodies that declare kWriteThrough (dl_unpack_sgd_q8). `make TUNING=1`
+// DL_TUNE_AUTO selects: non-temporal loads with plain or non-temporal stores. `make TUNING=1`
 // (-DDL_TUNING) instantiates the whole matrix -- plain loads, write-through for every body --
 // for the measurement tools (tools/cold_sweep.py); dl_tree_tune rejects the rest otherwise.
 template <class Body, bool NTL, int NTS>
@@ -214,13 +213,6 @@ hipError_t launch_pairs(const Launch& L, const Body& body, int32_t grid) {
 
 #endif  // DL_TUNING
 
-// bodies whose AUTO policy stores write-through declare kWriteThrough = true
-template <class B, class = void>
-struct write_through : std::false_type {};
-template <class B>
-struct write_through<B, std::void_t<decltype(B::kWriteThrough)>>
-    : std::bool_constant<B::kWriteThrough> {};
-
 template <class Body>
 hipError_t run(const Launch& L, const Body& body) {
   const int32_t n = L.c1 - L.c0;
@@ -236,11 +228,8 @@ hipError_t run(const Launch& L, const Body& body) {
   }
   if (sp == kStWT) return launch_walk<Body, true, kStWT>(L, body, grid);
 #else
-  if (!ntl) return hipErrorInvalidValue;  // not instantiated (dl_tree_tune rejects it first)
-  if (sp == kStWT) {
-    if constexpr (write_through<Body>::value) return launch_walk<Body, true, kStWT>(L, body, grid);
-    else return hipErrorInvalidValue;
-  }
+  // not instantiated (dl_tree_tune rejects these flags first)
+  if (!ntl || sp == kStWT) return hipErrorInvalidValue;
 #endif
   if (sp == kStNT) return launch_walk<Body, true, kStNT>(L, body, grid);
   return launch_walk<Body, true, kStPlain>(L, body, grid);

@@ -142,7 +142,6 @@ struct UnpackSgdQ8 {
   float* mom;
   SgdArgs a;
   int inner_slot;
-  static constexpr bool kWriteThrough = true;  // its AUTO policy below 2^28 elements
   template <bool NTL, int NTS>
   __device__ __forceinline__ void run(const Chunk& ck, int c, void* const* caddr, int nchunk, int tid) const {
     float* in = inner_slot >= 0 ? slot_ptr<float>(caddr, nchunk, inner_slot, c) : nullptr;
