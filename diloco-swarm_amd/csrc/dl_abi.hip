@@ -381,12 +381,13 @@ constexpr int32_t kAutoDelta = DL_TUNE_NT_LOADS;
 constexpr int32_t kAutoOther = DL_TUNE_NT_LOADS;
 // int8 encoder: its one 16-B payload store per lane non-temporal (tools/q8_layout.hip)
 constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
-// Launches over more than 2^28 elements (1 GiB of fp32, four times the Infinity Cache): their
-// output cannot stay cached for the next kernel, so the kernels that store plainly at bucket
-// size (dl_delta_pack, dl_gather; dl_scatter and dl_unpack_avg also take two chunks per
-// workgroup there) store non-temporally -- cold over a whole T1.3B tree dl_delta_pack 3 %,
-// dl_gather 1 %, dl_scatter / dl_unpack_avg 7 % faster; at T125 / bucket size the same policy
-// is 2-8 % slower (tools/cold_sweep.py "auto", profiles/r02_cold_sweep_flags_auto_*.json).
+// The two producers (dl_delta_pack, dl_gather) store plainly below 2^28 elements: the bucket
+// they write is read next by RCCL or the unpack, from the Infinity Cache -- timed together with
+// the consumer and charged with the write-back, plain is 4.5-7 % faster than NT on T125
+// (tools/cold_sweep.py --what pipe --flushed, profiles/r03_pipe_flushed_t125.json). Over more
+// than 2^28 elements (1 GiB of fp32, four times the Infinity Cache) the output cannot stay
+// cached, so they store non-temporally (dl_scatter and dl_unpack_avg also take two chunks per
+// workgroup there: 6 % faster flushed, profiles/r03_cold_sweep_flushed_t13b.json).
 constexpr int32_t kBigLaunchChunks = (1 << 28) / DL_CHUNK_ELEMS;
 constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // Kernels whose output no kernel re-reads next (dl_scatter: the inner params; dl_unpack_avg:

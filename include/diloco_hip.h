@@ -103,9 +103,10 @@ DL_API int dl_tree_bind(dl_tree_t tree, int32_t slot, const uint64_t* dev_ptrs, 
                         dl_stream_t stream);
 /* Launch shape of every walker kernel on this tree: max_blocks caps the grid (0 = one
  * workgroup per chunk, the default); flags = DL_TUNE_AUTO (the default: the measured
- * per-kernel choice -- NT loads everywhere; NT stores in the SGD kernels and, over launches of
- * more than 2^28 elements, in dl_delta_pack / dl_gather / dl_scatter / dl_unpack_avg;
- * write-through stores in dl_unpack_sgd_q8 below that size) or DL_TUNE_NT_LOADS [|
+ * per-kernel choice -- NT loads everywhere; NT stores in the SGD kernels, dl_scatter,
+ * dl_unpack_avg and dl_unpack_sgd_q8, and in dl_delta_pack / dl_gather over launches of more
+ * than 2^28 elements; plain stores for those two producers below that size, where the next
+ * kernel or RCCL re-reads their output from the Infinity Cache) or DL_TUNE_NT_LOADS [|
  * DL_TUNE_NT_STORES] for every kernel. Plain loads, DL_TUNE_WT_STORES (write-through, sc1)
  * for every kernel and DL_TUNE_PAIRS exist only in the tuning build (make TUNING=1, dl_tuning_build() == 1);
  * the product library rejects them with DL_E_ARG. Results are identical for every setting;
