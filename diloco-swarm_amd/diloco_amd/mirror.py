@@ -456,6 +456,9 @@ class DeviceOuterMirror:
         self.d_wire16 = (torch.zeros(self.tree.total, dtype=torch.bfloat16, device=self.device)
                          if wire == "bf16" else None)
         self._sum16 = False  # the pending Σ is in d_wire16 (.grad's arena is stale)
+        # fused, N > 1: the bucket all_reduces sync_gradients left in flight (the SGD pass of
+        # bucket b waits for its own collective only, so it overlaps bucket b+1's)
+        self._works: Optional[list] = None
         # per-tensor views of each arena and their addresses, made once: the per-step checks
         # compare raw addresses (an outer step must not cost a Python tensor per parameter)
         self._views = {"theta": self._make_views(self.d_theta),
@@ -575,7 +578,8 @@ class DeviceOuterMirror:
     # ---- deferred work (fused mode) ------------------------------------------------------
     @property
     def pending(self) -> bool:
-        return self._delta is not None or self._div != 1 or self._sum16
+        return (self._delta is not None or self._div != 1 or self._sum16
+                or self._works is not None)
 
     def _take_delta(self, tver_now=None) -> List[torch.Tensor]:
         """The pending delta's inner params, checked unchanged since compute_pseudo_gradient
@@ -594,8 +598,15 @@ class DeviceOuterMirror:
         self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))
         return inner
 
+    def _join(self) -> None:
+        """The current stream waits for every collective still in flight on the wire."""
+        works, self._works = self._works, None
+        for w in works or ():
+            w.wait()
+
     def settle_grads(self) -> None:
         """Complete the pending work so the packed .grad holds the reference's values."""
+        self._join()
         if self._delta is not None:
             self._take_delta()
             self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
@@ -624,6 +635,7 @@ class DeviceOuterMirror:
     def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
         """outer.grad = outer - inner (src/utils.py:218-221); .grad are views of d_wire."""
         inner = list(inner_params)
+        self._join()  # a collective still reading / writing the wire finishes first
         tver = self._relay_theta()
         iptrs = _ptrs(inner)
         self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))
@@ -651,7 +663,7 @@ class DeviceOuterMirror:
             def pack(b):
                 self.k.delta_pack(self.tree, b, SLOT_INNER, self.d_theta, self.d_wire)
         else:
-            if self._div != 1:
+            if self.pending:
                 self.settle_grads()  # a second sync_gradients reduces the averages
             self._relay_grads(zero_fill_missing=True)
 
@@ -659,14 +671,15 @@ class DeviceOuterMirror:
             lo, hi = self.tree.bucket_ranges[b]
             return self.d_wire[lo:hi]
 
-        div = num_peers if self.fused else 1
+        if self.fused:  # every bucket's collective in flight; the SGD pass waits per bucket
+            self._launch_reductions(pack, view, group)
+            self._div = num_peers
+            return
         pipelined_buckets(
             self.tree.n_buckets, pack or (lambda b: None),
             lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
-            (lambda b: None) if self.fused else
-            (lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire)),
+            lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
         )
-        self._div = div
 
     def _all_reduce_bf16(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
         """The bf16 wire: per bucket, the deltas (a pending delta: dl_delta_pack straight to
@@ -695,14 +708,27 @@ class DeviceOuterMirror:
             lo, hi = self.tree.bucket_ranges[b]
             return w16[lo:hi]
 
+        if self.fused:
+            self._launch_reductions(pack, view, group)
+            self._div, self._sum16 = num_peers, True
+            return
         pipelined_buckets(
             self.tree.n_buckets, pack,
             lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
-            (lambda b: None) if self.fused else
-            (lambda b: self.k.unpack_avg(self.tree, b, w16, num_peers, -1, self.d_wire)),
+            lambda b: self.k.unpack_avg(self.tree, b, w16, num_peers, -1, self.d_wire),
         )
-        if self.fused:
-            self._div, self._sum16 = num_peers, True
+
+    def _launch_reductions(self, pack, view, group) -> None:
+        """Fused N > 1: pack(b) then an asynchronous all_reduce(SUM) of bucket b, for every
+        bucket, none waited for here (OuterSGD.step waits bucket by bucket, anything that reads
+        or rewrites the wire first joins them all)."""
+        works = []
+        for b in range(self.tree.n_buckets):
+            if pack is not None:
+                pack(b)
+            works.append(dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group,
+                                         async_op=True))
+        self._works = works
 
     def sgd_step(self, lr: float, momentum: float, nesterov: bool,
                  host_bufs: Optional[List[Optional[torch.Tensor]]]) -> List[Optional[torch.Tensor]]:
@@ -749,9 +775,17 @@ class DeviceOuterMirror:
             if write:
                 self.k.bind(self.tree, SLOT_INNER, target[0], self.device, key=tuple(target[1]))
             # a pending /n stays pending: the wire keeps the Σ, .grad settles it when read
-            self.k.unpack_sgd(self.tree, ALL, self.d_wire16 if self._sum16 else self.d_wire,
-                              self._div, self.d_theta, mom, lr, momentum, nesterov, first,
-                              SLOT_INNER if write else -1)
+            wire = self.d_wire16 if self._sum16 else self.d_wire
+            slot = SLOT_INNER if write else -1
+            works, self._works = self._works, None
+            if works is None:
+                self.k.unpack_sgd(self.tree, ALL, wire, self._div, self.d_theta, mom, lr,
+                                  momentum, nesterov, first, slot)
+            else:  # bucket b's SGD waits for bucket b's collective only
+                for b, w in enumerate(works):
+                    w.wait()
+                    self.k.unpack_sgd(self.tree, b, wire, self._div, self.d_theta, mom, lr,
+                                      momentum, nesterov, first, slot)
         self._synced = (target + (tver,)) if write else None
         return bufs
 
@@ -776,4 +810,5 @@ class DeviceOuterMirror:
             self._synced = (inner, iptrs, _vers(inner), tver)
 
     def close(self) -> None:
+        self._join()
         self.tree.close()

@@ -54,6 +54,7 @@ from .kernels import default_kernels
 from .mirror import (OUTER_WIRES, WRITE_BACKS, DeviceOuterMirror, HostOuterMirror,
                      module_params)
 from .optim import OuterSGD
+from .plan import DEFAULT_BUCKET_CAP_ELEMS
 
 _ATTR = "_diloco_mirror"
 _OUTER = "_diloco_outer"
@@ -85,7 +86,8 @@ def outer_mirror(outer_model: nn.Module, device=None):
             p = next(outer_model.parameters(), None)
             if p is None:
                 raise ValueError("outer model has no parameters")
-            m = DeviceOuterMirror(outer_model, p.device, kernels=k,
+            cap = int(os.environ.get("DILOCO_OUTER_BUCKET_ELEMS", DEFAULT_BUCKET_CAP_ELEMS))
+            m = DeviceOuterMirror(outer_model, p.device, kernels=k, bucket_cap_elems=cap,
                                   fused=getattr(outer_model, _FUSED, False),
                                   wire=getattr(outer_model, _WIRE, "f32"))
             object.__setattr__(outer_model, _ATTR, m)

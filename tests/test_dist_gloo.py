@@ -73,13 +73,15 @@ def _worker(rank, world, port, mode, num_stages, out):
     rec = {}
     if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_host",
                 "dropin_device_quiet", "dropin_device_eager", "dropin_device_bf16",
-                "dropin_device_bf16_eager"):
+                "dropin_device_bf16_eager", "dropin_device_quiet_buckets"):
+        if mode == "dropin_device_quiet_buckets":  # the exchange in several buckets: the SGD
+            os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # pass waits bucket by bucket
         from diloco_amd.utils import flush_outer_model, has_mirror
 
         deferred = mode == "dropin_deferred"
         # quiet: nothing reads the outer model between the four calls (src/train.py:261-269),
         # so the fused device model defers the delta and the /n into its one SGD pass
-        quiet = mode in ("dropin_device_quiet", "dropin_device_bf16")
+        quiet = mode in ("dropin_device_quiet", "dropin_device_bf16", "dropin_device_quiet_buckets")
         device = mode.startswith("dropin_device")
         inner = _micro_module(theta0, shapes)
         outer = get_outer_model(inner, placement="device" if device else None,
@@ -96,6 +98,8 @@ def _worker(rank, world, port, mode, num_stages, out):
                 "DeviceOuterMirror" if device else "HostOuterMirror")
             if device:
                 assert outer_mirror(outer).fused == (not mode.endswith("_eager"))
+                if mode.endswith("_buckets"):
+                    assert outer_mirror(outer).tree.n_buckets > 2
         comm = TrainingComm(world_, (1, 1, 32), None)
         for s in range(1, MICRO_STEPS + 1):
             prev = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
@@ -285,6 +289,7 @@ def _run(mode, world, num_stages=1):
 
 
 @pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_device_quiet",
+                                  "dropin_device_quiet_buckets",
                                   "dropin_device_eager", "dropin_deferred", "engine",
                                   "engine_ar", "engine_a2a", "dropin_host"])
 def test_two_peers_match_reference_bit_exact(mode):
@@ -297,14 +302,15 @@ def test_two_peers_match_reference_bit_exact(mode):
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
             if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
-    if mode.startswith("dropin") and mode != "dropin_device_quiet":
+    if mode.startswith("dropin") and not mode.startswith("dropin_device_quiet"):
         assert recs[0]["delta_s1"].tobytes() == g["delta_s1_r0"].tobytes()
         assert recs[1]["delta_s1"].tobytes() == g["delta_s1_rlast"].tobytes()
 
 
 @pytest.mark.parametrize("mode,world", [("dropin", 4), ("engine", 4), ("engine_ar", 4),
                                         ("dropin", 8), ("engine", 8), ("dropin_host", 4),
-                                        ("dropin_device_quiet", 4)])
+                                        ("dropin_device_quiet", 4),
+                                        ("dropin_device_quiet_buckets", 4)])
 def test_four_and_eight_peers_match_reference_normwise(mode, world):
     """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""
     from diloco_amd.trees import get_tree
