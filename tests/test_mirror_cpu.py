@@ -302,3 +302,37 @@ def test_fused_outer_parameters_share_one_version_counter_and_flag_assignments()
     for p, b in zip(ps, before):
         assert torch.equal(p.detach(), b - 0.5 * 0.25)
         assert p.grad.data_ptr() != 0 and torch.equal(p.grad, torch.full_like(p, 0.25))
+
+
+def test_fused_outer_sgd_with_lr_scheduler_and_step_hooks():
+    """OuterSGD runs torch.optim's step hooks itself (it skips only the profiler annotation
+    when no profiler runs): an LR scheduler between outer steps and pre / post hooks behave as
+    on torch.optim.SGD; θ follows the oracle with the scheduled learning rates."""
+    import warnings
+
+    from oracle import oracle
+
+    inner, outer = _device_models(True)
+    opt = get_optimizer(outer, SGD_CFG)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+    calls = []
+    h1 = opt.register_step_pre_hook(lambda o, a, k: calls.append("pre"))
+    h2 = opt.register_step_post_hook(lambda o, a, k: calls.append("post"))
+    theta = [p.detach().numpy().reshape(-1).copy() for p in outer.parameters()]
+    buf = [np.empty_like(t) for t in theta]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # e.g. "lr_scheduler.step() before optimizer.step()"
+        for s, lr in ((1, 0.7), (2, 0.35)):
+            _set_inner(inner, outer, s)
+            inners = [p.detach().numpy().reshape(-1).copy() for p in inner.parameters()]
+            compute_pseudo_gradient(inner, outer)
+            opt.step()
+            sync_inner_model(outer, inner)
+            sched.step()
+            for t in range(len(theta)):
+                oracle.sgd(theta[t], buf[t], oracle.delta(theta[t], inners[t]), lr, 0.9, True,
+                           s == 1)
+            assert _host(outer.parameters()).tobytes() == np.concatenate(theta).tobytes(), s
+    assert calls == ["pre", "post", "pre", "post"]
+    h1.remove()
+    h2.remove()
