@@ -495,3 +495,61 @@ def test_t125_fused_device_dropin_bit_exact_vs_oracle():
             buf = opt.state[p]["momentum_buffer"].cpu().numpy().reshape(-1)
             assert buf.tobytes() == st.buf[t].tobytes(), (s, t)
             assert p.grad.cpu().numpy().reshape(-1).tobytes() == delta[t].tobytes(), (s, t)
+
+
+def test_t13b_fused_device_dropin_vs_oracle_on_sampled_tensors():
+    """The reference's four calls at the 1.3B workload (292 tensors, 1,313,722,368 params) on
+    the fused device outer model, one peer, 2 outer steps, nothing read in between: θ, the
+    momentum, .grad and the inner params bit-exact vs the C oracle on a 4 Mi window of wte,
+    block 0's tensors and the last tensor (every step is elementwise, so a window is
+    restated exactly from the counter-based inputs)."""
+    import gc
+
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from oracle import oracle
+
+    spec = get_tree("t1.3b")
+    numels, init = spec.numels(), spec.init_spec()
+    picks = [(0, 37_000_011, 4 << 20)] + [(t, 0, numels[t]) for t in range(1, 10)] + [
+        (len(numels) - 1, 0, numels[-1])]
+    shapes = [s for _, s in spec.params()]
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList(
+        [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"),
+                                                       shapes)])
+    outer = get_outer_model(inner, "device")
+    assert outer._diloco_mirror.fused and outer._diloco_mirror.tree.n_buckets == 25
+    opt = get_optimizer(outer, SGD_CFG)
+    F32 = np.float32
+    exp = {}
+    for t, lo, m in picks:
+        b, sc = init[t]
+        exp[t] = [(F32(b) + synth.uniform(synth.OUTER_SEED, t, m, start=lo) * F32(sc)).astype(F32),
+                  np.empty(m, dtype=F32)]
+    ps, qs = list(outer.parameters()), list(inner.parameters())
+    for s in (1, 2):
+        synth.inner_tree_device([p.detach().view(-1) for p in ps], s, 0,
+                                out=[q.data.view(-1) for q in qs])
+        compute_pseudo_gradient(inner, outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        for t, lo, m in picks:
+            th, buf = exp[t]
+            x = (F32(0.0) + synth.uniform(synth.noise_seed(s, 0), t, m, start=lo)
+                 * F32(synth.NOISE_SCALE) + th).astype(F32)
+            g = oracle.delta(th, x)
+            oracle.sgd(th, buf, g, 0.7, 0.9, True, s == 1)
+            got = ps[t].detach().reshape(-1)[lo:lo + m].cpu().numpy()
+            assert got.tobytes() == th.tobytes(), (s, t)
+            assert qs[t].detach().reshape(-1)[lo:lo + m].cpu().numpy().tobytes() == th.tobytes()
+            mb = opt.state[ps[t]]["momentum_buffer"].reshape(-1)[lo:lo + m].cpu().numpy()
+            assert mb.tobytes() == buf.tobytes(), (s, t)
+            assert ps[t].grad.reshape(-1)[lo:lo + m].cpu().numpy().tobytes() == g.tobytes()
+    outer._diloco_mirror.close()
+    del outer, inner, opt, ps, qs
+    gc.collect()
+    torch.cuda.empty_cache()
