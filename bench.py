@@ -1450,7 +1450,9 @@ class _Emitter:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50,
+                    help="timed steps K (the first timed step also carries the host's issue of "
+                         "its calls after the barrier: 1/K of the per-step figure)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--tree", default="t125")
     ap.add_argument("--wire", default="f32", choices=["f32", "bf16"])
