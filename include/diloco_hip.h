@@ -219,7 +219,8 @@ DL_API int dl_shard_reduce_avg(const void* slices, int32_t wire_dtype, int32_t n
 
 /* ---- int8 wire codec (not in the reference) --------------------------
  * One DL_Q8_SLOT_BYTES slot per chunk of the bucket, in chunk order: fp32 scale at byte 0,
- * int8 values at byte 64 (bytes past the chunk's length stay zero; slots must be zeroed once).
+ * zeros to byte 64 (the encoder and the reduce write the whole header), int8 values at byte
+ * 64 (bytes past the chunk's length stay zero; slots must be zeroed once).
  * Quantiser: s = amax/127, q = s == 0 ? 0 : clamp(rint(x/s), -127, 127), value q*s.
  * dl_delta_q8:      slots <- quantise(outer - inner) per chunk  (a2, 8 B read + 1.02 B written)
  * dl_q8_reduce:     out[j] <- quantise((sum_r deq(recv[r][j])) / divisor), r in rank order;
