@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(T) q8enc(const float* th, const float* in, uns
 
 // the payload staged through LDS, then one 16-B store per lane (1 KB per wave instruction
 // instead of four 256-B ones); NTS: non-temporal payload stores
-template <int SLOT, int HDR, bool SPLIT, bool NTS>
+template <int SLOT, int HDR, bool SPLIT, bool NTS, bool FULLHDR = false>
 __global__ void __launch_bounds__(T) q8lds(const float* th, const float* in, unsigned char* slots,
                                            float* scales) {
   __shared__ unsigned stage[CH / 4];
@@ -132,7 +132,13 @@ __global__ void __launch_bounds__(T) q8lds(const float* th, const float* in, uns
   G u4* q = (G u4*)(slot + HDR);
   if constexpr (NTS) __builtin_nontemporal_store(v, q + threadIdx.x);
   else q[threadIdx.x] = v;
-  if (threadIdx.x == 0) {
+  if constexpr (FULLHDR && !SPLIT) {  // the whole header, scale then zeros, as 16-B stores
+    if (threadIdx.x < HDR / 16) {
+      const u4 h = {threadIdx.x == 0 ? __float_as_uint(s) : 0u, 0u, 0u, 0u};
+      if constexpr (NTS) __builtin_nontemporal_store(h, (G u4*)slot + threadIdx.x);
+      else ((G u4*)slot)[threadIdx.x] = h;
+    }
+  } else if (threadIdx.x == 0) {
     if (SPLIT) scales[blockIdx.x] = s;
     else *(G float*)slot = s;
   }
@@ -239,6 +245,7 @@ int main(int argc, char** argv) {
   ADD("q8_split_nobar               ", q8b, hipLaunchKernelGGL((q8enc<4096, 0, true, true, false>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds     4160, 16-B stores ", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, false>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_nt  4160, NT 16-B     ", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, true>), g, b, 0, 0, th, in, slots, scales));
+  ADD("q8_lds_nt_fullhdr (product) ", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, true, true>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_split 4096+scales     ", q8b, hipLaunchKernelGGL((q8lds<4096, 0, true, false>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_split_nt              ", q8b, hipLaunchKernelGGL((q8lds<4096, 0, true, true>), g, b, 0, 0, th, in, slots, scales));
   unsigned short* wb = reinterpret_cast<unsigned short*>(w);
