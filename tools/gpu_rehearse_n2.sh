@@ -2,7 +2,7 @@
 # (RCCL refuses two ranks per device; the driver's multi-GPU runs use RCCL).
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
-DILOCO_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+DILOCO_BENCH_BACKEND=gloo timeout -k 10 ${TO:-400} python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 ${EXTRA:---extra-tree none} \
   > gpurun_out/bench_n2_gloo.json 2> gpurun_out/bench_n2_gloo.err || { echo n2 rehearsal failed; tail -30 gpurun_out/bench_n2_gloo.err; exit 1; }
 cat gpurun_out/bench_n2_gloo.json
