@@ -303,9 +303,72 @@ def _worker(rank, world, port, mode, out):
         torch.cuda.synchronize()
         rec["got"] = _flat(p.grad for p in m.parameters())
         rec["ref"] = _flat(ref)
+    elif mode == "dropin_device_t125":
+        rec = _t125_dropin_two_peers(rank, world)
     np.savez(os.path.join(out, f"{mode}_r{rank}.npz"), **rec)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _t125_dropin_two_peers(rank, world, steps=2):
+    """This process = DP rank `rank` of `world` on the full T125 tree: the reference's four
+    calls (src/train.py:263-269, nothing read in between) on the fused device outer model,
+    the exchange over the gloo DP group in 256 MiB buckets. Checked in the worker against the
+    C oracle on sampled tensors (wte whole, the first block, the last tensor): θ, the momentum,
+    the inner params and `.grad` (the average) after each outer step; returns the mismatches."""
+    from diloco_amd import synth
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+    from oracle import oracle
+    from test_configs_gpu import _picks, _slice_inputs
+
+    F32 = np.float32
+    spec = get_tree("t125")
+    picks = _picks(True, spec)
+    init = spec.init_spec()
+    exp = {}
+    for t, lo, m in picks:  # the oracle on the sampled tensors: θ, buf and g per step
+        b, sc = init[t]
+        th = (F32(b) + synth.uniform(synth.OUTER_SEED, t, m, start=lo) * F32(sc)).astype(F32)
+        buf = np.empty_like(th)
+        for s in range(1, steps + 1):
+            g = oracle.sum_avg([oracle.delta(th, x)
+                                for x in _slice_inputs(t, lo, m, s, world, th)])
+            oracle.sgd(th, buf, g, 0.7, 0.9, True, s == 1)
+            exp[(t, s)] = (th.copy(), buf.copy(), g)
+    shapes = [sh for _, sh in spec.params()]
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList(
+        [torch.nn.Parameter(x.view(sh)) for x, sh in zip(synth.outer_tree_device(spec, "cuda:0"),
+                                                          shapes)])
+    outer = get_outer_model(inner, "device")  # fused (the default)
+    assert outer._diloco_mirror.fused and outer._diloco_mirror.tree.n_buckets >= 2
+    opt = get_optimizer(outer, SGD_CFG)
+    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    bad = []
+    for s in range(1, steps + 1):
+        th = [p.detach().view(-1) for p in outer.parameters()]
+        synth.inner_tree_device(th, s, rank, out=[p.data.view(-1) for p in inner.parameters()])
+        compute_pseudo_gradient(inner, outer)
+        comm.sync_gradients(outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        ops, ips = list(outer.parameters()), list(inner.parameters())
+        for t, lo, m in picks:
+            want_th, want_buf, want_g = exp[(t, s)]
+            got = {"theta": ops[t].detach().view(-1)[lo:lo + m],
+                   "buf": opt.state[ops[t]]["momentum_buffer"].view(-1)[lo:lo + m],
+                   "inner": ips[t].detach().view(-1)[lo:lo + m],
+                   "grad": ops[t].grad.view(-1)[lo:lo + m]}
+            for k, want in (("theta", want_th), ("buf", want_buf), ("inner", want_th),
+                            ("grad", want_g)):
+                if got[k].cpu().numpy().tobytes() != want.tobytes():
+                    bad.append(f"step {s} tensor {t} {k}")
+    return {"bad": np.array(bad or ["none"]), "checked": np.int64(len(picks) * steps)}
 
 
 def _run(mode, world=2):  # noqa: D401
@@ -326,6 +389,18 @@ def test_two_peers_on_gpu_match_reference(mode):
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (mode, s)
             if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
+
+
+def test_t125_two_peers_dropin_device_bit_exact_vs_oracle():
+    """BASELINE config #3 (T125, DP = 2, fp32) through the reference's own calls at full size:
+    two processes, the fused device outer model (the bench's headline path at N > 1: per
+    bucket dl_delta_pack -> all_reduce, then one dl_unpack_sgd pass with /n and the inner
+    write), 2 outer steps. θ, momentum, inner and .grad bit-exact against the C oracle on wte
+    (38.6 M elements, whole), the first block and the last tensor (src/comm.py:122-123,
+    src/utils.py:221,226)."""
+    for rec in _run("dropin_device_t125"):
+        assert rec["checked"] == 22
+        assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
 
 
 def test_two_peers_on_gpu_bf16_outer_wire():
