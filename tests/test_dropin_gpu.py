@@ -303,19 +303,52 @@ def _worker(rank, world, port, mode, out):
         torch.cuda.synchronize()
         rec["got"] = _flat(p.grad for p in m.parameters())
         rec["ref"] = _flat(ref)
-    elif mode == "dropin_device_t125":
-        rec = _t125_dropin_two_peers(rank, world)
+    elif mode == "dp_t125":
+        # the per-step DP sync (src/train.py:249-251 -> src/comm.py:117-123) on device grads of
+        # the full T125 shapes: GradSync (dl_gather -> all_reduce -> dl_unpack_avg, 256 MiB
+        # buckets) against torch's own per-tensor all_reduce + /n of the same grads
+        from diloco_amd import synth
+        from diloco_amd.comm import TrainingComm
+        from diloco_amd.trees import get_tree
+        from diloco_amd.world import World
+
+        spec = get_tree("t125")
+        m = torch.nn.Module()
+        m.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(sh, device="cuda:0"))
+                                       for _, sh in spec.params()])
+        grads = synth.inner_tree_device(synth.outer_tree_device(spec, "cuda:0"), 3, rank)
+        for p, g in zip(m.parameters(), grads):
+            p.grad = g.view(p.shape)
+        ref = [p.grad.clone() for p in m.parameters()]
+        for r in ref:
+            dist.all_reduce(r, op=dist.ReduceOp.SUM)
+            r /= world
+        comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+        comm.sync_gradients(m)
+        torch.cuda.synchronize()
+        bad = [i for i, (p, r) in enumerate(zip(m.parameters(), ref))
+               if not torch.equal(p.grad, r)]
+        rec["bad"] = np.array(bad or [-1])
+        rec["n"] = np.int64(len(ref))
+    elif mode in ("dropin_device_t125", "dropin_device_t125_bf16", "dropin_device_t13b"):
+        rec = _full_size_dropin_two_peers(rank, world,
+                                          wire="bf16" if mode.endswith("bf16") else "f32",
+                                          tree="t1.3b" if mode.endswith("t13b") else "t125")
     np.savez(os.path.join(out, f"{mode}_r{rank}.npz"), **rec)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _t125_dropin_two_peers(rank, world, steps=2):
-    """This process = DP rank `rank` of `world` on the full T125 tree: the reference's four
-    calls (src/train.py:263-269, nothing read in between) on the fused device outer model,
-    the exchange over the gloo DP group in 256 MiB buckets. Checked in the worker against the
-    C oracle on sampled tensors (wte whole, the first block, the last tensor): θ, the momentum,
-    the inner params and `.grad` (the average) after each outer step; returns the mismatches."""
+def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125"):
+    """This process = DP rank `rank` of `world` on a full tree (T125, or T1.3B in 25 buckets):
+    the reference's four calls (src/train.py:263-269, nothing read in between) on the fused
+    device outer model, the exchange over the gloo DP group in 256 MiB buckets. Checked in the
+    worker against the C oracle on sampled tensors (wte whole on T125, a 4 Mi-element window of
+    it on T1.3B, the first block, the last tensor): θ, the momentum,
+    the inner params and `.grad` (the average) after each outer step; returns the mismatches.
+    wire="bf16" (config #5's codec behind the same calls): the oracle's restatement of the
+    codec -- each delta rounded to bf16 (RNE), the partial sums rounded to bf16 in rank order,
+    the average = sum / n in fp32."""
     from diloco_amd import synth
     from diloco_amd.comm import TrainingComm
     from diloco_amd.trees import get_tree
@@ -326,8 +359,8 @@ def _t125_dropin_two_peers(rank, world, steps=2):
     from test_configs_gpu import _picks, _slice_inputs
 
     F32 = np.float32
-    spec = get_tree("t125")
-    picks = _picks(True, spec)
+    spec = get_tree(tree)
+    picks = _picks(tree == "t125", spec)
     init = spec.init_spec()
     exp = {}
     for t, lo, m in picks:  # the oracle on the sampled tensors: θ, buf and g per step
@@ -335,8 +368,14 @@ def _t125_dropin_two_peers(rank, world, steps=2):
         th = (F32(b) + synth.uniform(synth.OUTER_SEED, t, m, start=lo) * F32(sc)).astype(F32)
         buf = np.empty_like(th)
         for s in range(1, steps + 1):
-            g = oracle.sum_avg([oracle.delta(th, x)
-                                for x in _slice_inputs(t, lo, m, s, world, th)])
+            d = [oracle.delta(th, x) for x in _slice_inputs(t, lo, m, s, world, th)]
+            if wire == "bf16":
+                acc = oracle.bf16_round(d[0])
+                for dr in d[1:]:
+                    acc = oracle.bf16_round((acc + oracle.bf16_round(dr)).astype(F32))
+                g = (acc / F32(world)).astype(F32)
+            else:
+                g = oracle.sum_avg(d)
             oracle.sgd(th, buf, g, 0.7, 0.9, True, s == 1)
             exp[(t, s)] = (th.copy(), buf.copy(), g)
     shapes = [sh for _, sh in spec.params()]
@@ -344,8 +383,9 @@ def _t125_dropin_two_peers(rank, world, steps=2):
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(x.view(sh)) for x, sh in zip(synth.outer_tree_device(spec, "cuda:0"),
                                                           shapes)])
-    outer = get_outer_model(inner, "device")  # fused (the default)
-    assert outer._diloco_mirror.fused and outer._diloco_mirror.tree.n_buckets >= 2
+    outer = get_outer_model(inner, "device", wire=wire)  # fused (the default)
+    assert outer._diloco_mirror.fused
+    assert outer._diloco_mirror.tree.n_buckets == (25 if tree == "t1.3b" else 2)
     opt = get_optimizer(outer, SGD_CFG)
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     bad = []
@@ -399,6 +439,35 @@ def test_t125_two_peers_dropin_device_bit_exact_vs_oracle():
     (38.6 M elements, whole), the first block and the last tensor (src/comm.py:122-123,
     src/utils.py:221,226)."""
     for rec in _run("dropin_device_t125"):
+        assert rec["checked"] == 22
+        assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
+
+
+def test_t125_two_peers_dp_grad_sync_matches_torch_all_reduce():
+    """§8f row 1 at full T125 size, two processes: TrainingComm.sync_gradients on device grads
+    (GradSync: dl_gather -> all_reduce per 256 MiB bucket -> dl_unpack_avg) equals torch's own
+    per-tensor all_reduce(SUM) / n of the same grads, every one of the 148 tensors bit-exact."""
+    for rec in _run("dp_t125"):
+        assert rec["n"] == 148
+        assert list(rec["bad"]) == [-1], list(rec["bad"])[:10]
+
+
+def test_t13b_two_peers_dropin_device_bit_exact_vs_oracle():
+    """BASELINE config #4's 1.3B workload (25 buckets, each packed right before its collective,
+    bucket b's SGD pass waiting for bucket b's exchange only) through the reference's four
+    calls, two processes: θ, momentum, inner and .grad bit-exact against the C oracle on a wte
+    window, block 0 and the last tensor after each of 2 outer steps."""
+    for rec in _run("dropin_device_t13b"):
+        assert rec["checked"] == 22
+        assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
+
+
+def test_t125_two_peers_dropin_device_bf16_wire_vs_codec_restatement():
+    """BASELINE config #5's codec (bf16 wire, SGD fused into the unpack) through the
+    reference's four calls at full T125 size, two processes: θ, momentum, inner and .grad (the
+    decoded average) bit-exact against the oracle's restatement of the codec on wte (whole),
+    block 0 and the last tensor after each of 2 outer steps."""
+    for rec in _run("dropin_device_t125_bf16"):
         assert rec["checked"] == 22
         assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
 
