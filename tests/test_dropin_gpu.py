@@ -330,10 +330,11 @@ def _worker(rank, world, port, mode, out):
                if not torch.equal(p.grad, r)]
         rec["bad"] = np.array(bad or [-1])
         rec["n"] = np.int64(len(ref))
-    elif mode in ("dropin_device_t125", "dropin_device_t125_bf16", "dropin_device_t13b"):
+    elif mode in ("dropin_device_t125", "dropin_device_t125_bf16", "dropin_device_t13b",
+                  "dropin_device_t13b_n8"):
         rec = _full_size_dropin_two_peers(rank, world,
                                           wire="bf16" if mode.endswith("bf16") else "f32",
-                                          tree="t1.3b" if mode.endswith("t13b") else "t125")
+                                          tree="t1.3b" if "t13b" in mode else "t125")
     np.savez(os.path.join(out, f"{mode}_r{rank}.npz"), **rec)
     dist.barrier()
     dist.destroy_process_group()
@@ -346,6 +347,9 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125"):
     worker against the C oracle on sampled tensors (wte whole on T125, a 4 Mi-element window of
     it on T1.3B, the first block, the last tensor): θ, the momentum,
     the inner params and `.grad` (the average) after each outer step; returns the mismatches.
+    Bit-exact at two peers; beyond, gloo's summation order differs from the oracle's rank
+    order, so per tensor |got - oracle| <= 1e-6 * max|oracle|, and every rank's
+    values are returned as a digest for the replicas to be compared bit for bit.
     wire="bf16" (config #5's codec behind the same calls): the oracle's restatement of the
     codec -- each delta rounded to bf16 (RNE), the partial sums rounded to bf16 in rank order,
     the average = sum / n in fp32."""
@@ -356,6 +360,9 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125"):
                                   sync_inner_model)
     from diloco_amd.world import World
     from oracle import oracle
+    import hashlib
+
+    from conftest import normwise_ok
     from test_configs_gpu import _picks, _slice_inputs
 
     F32 = np.float32
@@ -389,6 +396,7 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125"):
     opt = get_optimizer(outer, SGD_CFG)
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     bad = []
+    digest = hashlib.sha256()
     for s in range(1, steps + 1):
         th = [p.detach().view(-1) for p in outer.parameters()]
         synth.inner_tree_device(th, s, rank, out=[p.data.view(-1) for p in inner.parameters()])
@@ -406,9 +414,14 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125"):
                    "grad": ops[t].grad.view(-1)[lo:lo + m]}
             for k, want in (("theta", want_th), ("buf", want_buf), ("inner", want_th),
                             ("grad", want_g)):
-                if got[k].cpu().numpy().tobytes() != want.tobytes():
+                g = got[k].cpu().numpy()
+                digest.update(g.tobytes())
+                ok = (g.tobytes() == want.tobytes() if world <= 2
+                      else normwise_ok(g, want, 1e-6))
+                if not ok:
                     bad.append(f"step {s} tensor {t} {k}")
-    return {"bad": np.array(bad or ["none"]), "checked": np.int64(len(picks) * steps)}
+    return {"bad": np.array(bad or ["none"]), "checked": np.int64(len(picks) * steps),
+            "digest": np.array(digest.hexdigest())}
 
 
 def _run(mode, world=2):  # noqa: D401
@@ -460,6 +473,19 @@ def test_t13b_two_peers_dropin_device_bit_exact_vs_oracle():
     for rec in _run("dropin_device_t13b"):
         assert rec["checked"] == 22
         assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
+
+
+def test_t13b_eight_peers_dropin_device_vs_oracle():
+    """BASELINE config #4 itself (1.3B, DP = 8, 25 buckets pipelined) through the reference's
+    four calls with eight processes on the one GPU (gloo DP group on the device tensors, ~21 GB
+    of HBM each): θ, momentum, inner and .grad within 1e-6 normwise of the C oracle's
+    rank-order result on a wte window, block 0 and the last tensor after each of 2 outer
+    steps, and all eight replicas bit-identical."""
+    recs = _run("dropin_device_t13b_n8", 8)
+    for rec in recs:
+        assert rec["checked"] == 22
+        assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
+    assert len({str(rec["digest"]) for rec in recs}) == 1
 
 
 def test_t125_two_peers_dropin_device_bf16_wire_vs_codec_restatement():
