@@ -330,6 +330,8 @@ def _worker(rank, world, port, mode, out):
                if not torch.equal(p.grad, r)]
         rec["bad"] = np.array(bad or [-1])
         rec["n"] = np.int64(len(ref))
+    elif mode == "dropin_device_t13b_bf16_n8":
+        rec = _bf16_dropin_codec_check(rank, world)
     elif mode in ("dropin_device_t125", "dropin_device_t125_bf16", "dropin_device_t13b",
                   "dropin_device_t13b_n8"):
         rec = _full_size_dropin_two_peers(rank, world,
@@ -338,6 +340,81 @@ def _worker(rank, world, port, mode, out):
     np.savez(os.path.join(out, f"{mode}_r{rank}.npz"), **rec)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _bf16_dropin_codec_check(rank, world, steps=2, tree="t1.3b"):
+    """Config #5 (1.3B, bf16 wire, SGD fused into the unpack) through the reference's four calls
+    with `world` processes: the exchange's bf16 partial sums come in gloo's order, so instead of
+    a bit pattern each outer step checks, on sampled tensors (a wte window, block 0, the last
+    tensor) and from the θ / momentum the device held before the step, that (1) `.grad` (the
+    decoded average) is within the codec's a-priori bound (diloco_amd.outer.bf16_codec_bound,
+    replicated bf16 all-reduce in any order) of the fp32 average of the same deltas, and (2) θ,
+    the momentum and the inner params are torch's SGD-Nesterov applied to exactly that `.grad`
+    (bit-exact: the SGD pass consumes the decoded average). Returns mismatches, the worst
+    error / bound and a digest of the values for the replicas to be compared bit for bit."""
+    import hashlib
+
+    from diloco_amd import synth
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.outer import bf16_codec_bound
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+    from oracle import oracle
+    from test_configs_gpu import _picks, _slice_inputs
+
+    F32 = np.float32
+    spec = get_tree(tree)
+    picks = _picks(False, spec)
+    shapes = [sh for _, sh in spec.params()]
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList(
+        [torch.nn.Parameter(x.view(sh)) for x, sh in zip(synth.outer_tree_device(spec, "cuda:0"),
+                                                          shapes)])
+    outer = get_outer_model(inner, "device", wire="bf16")
+    opt = get_optimizer(outer, SGD_CFG)
+    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    bad, worst, digest = [], 0.0, hashlib.sha256()
+    ops, ips = list(outer.parameters()), list(inner.parameters())
+
+    def window(x, t, lo, m):
+        return x.detach().view(-1)[lo:lo + m].cpu().numpy()
+
+    for s in range(1, steps + 1):
+        before = {(t, lo): (window(ops[t], t, lo, m),
+                            None if s == 1 else window(opt.state[ops[t]]["momentum_buffer"], t, lo, m))
+                  for t, lo, m in picks}
+        th = [p.detach().view(-1) for p in ops]
+        synth.inner_tree_device(th, s, rank, out=[p.data.view(-1) for p in ips])
+        compute_pseudo_gradient(inner, outer)
+        comm.sync_gradients(outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        for t, lo, m in picks:
+            th0, buf0 = before[(t, lo)]
+            d = [oracle.delta(th0, x) for x in _slice_inputs(t, lo, m, s, world, th0)]
+            g32 = oracle.sum_avg(d)
+            bound = bf16_codec_bound(np.sum(np.abs(d), axis=0, dtype=np.float64), world,
+                                     "rccl").astype(F32)
+            g = window(ops[t].grad, t, lo, m)
+            err = np.abs(g.astype(np.float64) - g32)
+            if not np.all(err <= bound):
+                bad.append(f"step {s} tensor {t} codec bound")
+            worst = max(worst, float((err / np.maximum(bound, 1e-38)).max()))
+            th_exp, buf_exp = th0.copy(), (np.empty_like(th0) if buf0 is None else buf0.copy())
+            oracle.sgd(th_exp, buf_exp, g, 0.7, 0.9, True, s == 1)
+            for k, got in (("theta", window(ops[t], t, lo, m)),
+                           ("buf", window(opt.state[ops[t]]["momentum_buffer"], t, lo, m)),
+                           ("inner", window(ips[t], t, lo, m))):
+                digest.update(got.tobytes())
+                want = buf_exp if k == "buf" else th_exp
+                if got.tobytes() != want.tobytes():
+                    bad.append(f"step {s} tensor {t} {k}")
+            digest.update(g.tobytes())
+    return {"bad": np.array(bad or ["none"]), "checked": np.int64(len(picks) * steps),
+            "worst": np.float64(worst), "digest": np.array(digest.hexdigest())}
 
 
 def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125"):
@@ -486,6 +563,19 @@ def test_t13b_eight_peers_dropin_device_vs_oracle():
         assert rec["checked"] == 22
         assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
     assert len({str(rec["digest"]) for rec in recs}) == 1
+
+
+def test_t13b_eight_peers_dropin_device_bf16_wire_within_codec_bound():
+    """BASELINE config #5 itself (1.3B, DP = 8, bf16 wire, SGD fused into the unpack) through
+    the reference's four calls with eight processes on the one GPU: .grad within the codec's
+    a-priori bound of the fp32 average, θ / momentum / inner exactly torch's SGD-Nesterov of
+    that .grad, replicas bit-identical (see _bf16_dropin_codec_check)."""
+    recs = _run("dropin_device_t13b_bf16_n8", 8)
+    for rec in recs:
+        assert rec["checked"] == 22
+        assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
+    assert len({str(rec["digest"]) for rec in recs}) == 1
+    print(f"bf16 wire, 8 peers: worst codec error / bound {float(recs[0]['worst']):.3f}")
 
 
 def test_t125_two_peers_dropin_device_bf16_wire_vs_codec_restatement():
