@@ -326,8 +326,14 @@ def _worker(rank, world, port, mode, out):
         comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
         comm.sync_gradients(m)
         torch.cuda.synchronize()
-        bad = [i for i, (p, r) in enumerate(zip(m.parameters(), ref))
-               if not torch.equal(p.grad, r)]
+        if world <= 2:
+            bad = [i for i, (p, r) in enumerate(zip(m.parameters(), ref))
+                   if not torch.equal(p.grad, r)]
+        else:  # a bucket's all_reduce and a tensor's may add the peers in different orders
+            from conftest import normwise_ok
+
+            bad = [i for i, (p, r) in enumerate(zip(m.parameters(), ref))
+                   if not normwise_ok(p.grad.cpu().numpy(), r.cpu().numpy(), 1e-6)]
         rec["bad"] = np.array(bad or [-1])
         rec["n"] = np.int64(len(ref))
     elif mode == "dropin_device_t13b_bf16_n8":
@@ -538,6 +544,15 @@ def test_t125_two_peers_dp_grad_sync_matches_torch_all_reduce():
     (GradSync: dl_gather -> all_reduce per 256 MiB bucket -> dl_unpack_avg) equals torch's own
     per-tensor all_reduce(SUM) / n of the same grads, every one of the 148 tensors bit-exact."""
     for rec in _run("dp_t125"):
+        assert rec["n"] == 148
+        assert list(rec["bad"]) == [-1], list(rec["bad"])[:10]
+
+
+def test_t125_eight_peers_dp_grad_sync_matches_torch_all_reduce():
+    """The same with eight processes: every gradient within 1e-6 normwise of torch's own
+    per-tensor all_reduce / n (the peers' summation order may differ between a 256 MiB bucket
+    and a tensor)."""
+    for rec in _run("dp_t125", 8):
         assert rec["n"] == 148
         assert list(rec["bad"]) == [-1], list(rec["bad"])[:10]
 
