@@ -137,9 +137,10 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
         raise ValueError("the bf16 outer wire needs placement='device' (the host placement "
                          "keeps the reference's fp32 host tensors end to end)")
     outer_model = copy.deepcopy(inner_model)
+    has_params = next(inner_model.parameters(), None) is not None
     if placement == "host":
         outer_model = outer_model.to("cpu")
-    else:  # the inner model's GPU; the reference builds the outer model before moving the
+    elif has_params:  # the inner model's GPU; the reference builds the outer model before moving the
         # inner one (src/train.py:382), so a CPU inner model means the current device
         dev = _inner_device(inner_model)
         if dev.type == "cpu":
@@ -154,8 +155,9 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     object.__setattr__(outer_model, _WRITE_BACK, write_back)
     object.__setattr__(outer_model, _FUSED, bool(fused) and placement == "device")
     object.__setattr__(outer_model, _WIRE, wire)
-    if placement == "device":
-        # lay the parameters out in the packed HBM arena now (fused: as OuterParameters)
+    if placement == "device" and has_params:
+        # lay the parameters out in the packed HBM arena now (fused: as OuterParameters);
+        # a model without parameters keeps none: the four calls are the reference's empty loops
         outer_mirror(outer_model)
     elif write_back == "deferred":
         # a checkpoint of the outer model waits for the write-back in flight
@@ -173,9 +175,10 @@ def flush_outer_model(outer_model: nn.Module) -> None:
 
 
 def _host_path(inner_model: nn.Module, outer_model: nn.Module) -> bool:
-    """The reference's host semantics apply: a CPU inner model and no device mirror."""
+    """The reference's host semantics apply: a CPU inner model (or one without parameters,
+    for which the reference's loops run zero times) and no device mirror."""
     p = next(inner_model.parameters(), None)
-    return p is not None and not device_path(p) and not has_mirror(outer_model)
+    return (p is None or not device_path(p)) and not has_mirror(outer_model)
 
 
 def compute_pseudo_gradient(inner_model: nn.Module, outer_model: nn.Module) -> None:

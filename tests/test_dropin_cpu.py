@@ -70,3 +70,26 @@ def test_recv_thread_failure_wakes_a_blocked_receive():
     assert t.can_receive  # a training loop polling can_receive gets to the raise too
     with pytest.raises(ThreadStopped):
         t.receive()
+
+
+@pytest.mark.parametrize("placement", ["host", "device"])
+def test_parameterless_model_is_the_references_no_op(placement):
+    """A model without parameters: compute_pseudo_gradient and sync_inner_model are the
+    reference's loops over nothing (src/utils.py:218-226), and get_optimizer raises torch's own
+    error for an empty parameter list, as torch.optim.SGD does there (src/utils.py:62-63)."""
+    from types import SimpleNamespace
+
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+
+    inner = torch.nn.Sequential(torch.nn.ReLU())
+    outer = get_outer_model(inner, placement)
+    assert list(outer.parameters()) == []
+    compute_pseudo_gradient(inner, outer)
+    sync_inner_model(outer, inner)
+    cfg = SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True)
+    with pytest.raises(ValueError) as ours:
+        get_optimizer(outer, cfg)
+    with pytest.raises(ValueError) as theirs:
+        torch.optim.SGD(inner.parameters(), lr=0.7, momentum=0.9, nesterov=True)
+    assert str(ours.value) == str(theirs.value)
