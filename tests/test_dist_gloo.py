@@ -310,7 +310,8 @@ def test_two_peers_match_reference_bit_exact(mode):
 @pytest.mark.parametrize("mode,world", [("dropin", 4), ("engine", 4), ("engine_ar", 4),
                                         ("dropin", 8), ("engine", 8), ("dropin_host", 4),
                                         ("dropin_device_quiet", 4),
-                                        ("dropin_device_quiet_buckets", 4)])
+                                        ("dropin_device_quiet_buckets", 4),
+                                        ("dropin_device_quiet_buckets", 8)])
 def test_four_and_eight_peers_match_reference_normwise(mode, world):
     """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""
     from diloco_amd.trees import get_tree
