@@ -330,14 +330,24 @@ def module_params(model: torch.nn.Module) -> List[torch.nn.Parameter]:
     """list(model.parameters()), same order (modules in named_modules() order, each module's
     parameters in registration order, a shared parameter at its first occurrence), with the
     duplicates found by identity instead of Tensor.__hash__ (a Python call per lookup: the
-    per-call cost of the drop-in functions on a 148-tensor tree)."""
-    seen, out = set(), []
-    for mod in model.modules():
-        for p in mod._parameters.values():
-            if p is not None and id(p) not in seen:
-                seen.add(id(p))
-                out.append(p)
-    return out
+    per-call cost of the drop-in functions on a 148-tensor tree). The modules are walked here
+    as named_modules() walks them (pre-order, a shared module at its first occurrence) without
+    its generator chain and prefix strings, which were half of this function's time; the
+    duplicates go in one C-level dict build (keys keep their first position)."""
+    ps: list = []
+    mods: set = set()
+
+    def walk(m: torch.nn.Module) -> None:
+        mods.add(id(m))
+        ps.extend(m._parameters.values())
+        for c in m._modules.values():
+            if c is not None and id(c) not in mods:
+                walk(c)
+
+    walk(model)
+    uniq = dict(zip(map(id, ps), ps))
+    uniq.pop(id(None), None)  # parameters registered as None
+    return list(uniq.values())
 
 
 class OuterParameter(torch.nn.Parameter):

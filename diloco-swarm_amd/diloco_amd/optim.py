@@ -10,13 +10,15 @@ writes θ and the momentum buffers back to the host tensors the optimizer owns.
 from __future__ import annotations
 
 from itertools import chain
-from operator import is_
+from operator import is_, methodcaller
 
 import torch
 from torch.optim import SGD
 from torch.optim import optimizer as _optim
 
 from .mirror import HostOuterMirror
+
+_MOMENTUM_BUFFER = methodcaller("get", "momentum_buffer")
 
 
 class OuterSGD(SGD):
@@ -99,7 +101,7 @@ class OuterSGD(SGD):
         st = self.state
         same = len(st) == len(params) and all(map(is_, st.keys(), params))
         if same:
-            host_bufs = [v.get("momentum_buffer") for v in st.values()]
+            host_bufs = list(map(_MOMENTUM_BUFFER, st.values()))
         else:
             host_bufs = [st[p].get("momentum_buffer") for p in params]
         lr = g["lr"]
@@ -107,7 +109,9 @@ class OuterSGD(SGD):
             lr = float(lr.item())
         bufs = mirror.sgd_step(float(lr), momentum, bool(g["nesterov"]), host_bufs)
         if momentum != 0:
-            if same:
+            if same and all(map(is_, host_bufs, bufs)):
+                pass  # the state already holds these buffers (every step after the first)
+            elif same:
                 for v, b in zip(st.values(), bufs):
                     v["momentum_buffer"] = b
             else:

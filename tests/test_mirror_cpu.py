@@ -336,3 +336,32 @@ def test_fused_outer_sgd_with_lr_scheduler_and_step_hooks():
     assert calls == ["pre", "post", "pre", "post"]
     h1.remove()
     h2.remove()
+
+
+def test_module_params_is_parameters_order_by_identity():
+    """mirror.module_params (the drop-in calls' parameter walk) returns exactly
+    list(model.parameters()): pre-order modules, registration order, a tied parameter and a
+    module reachable twice at their first occurrence, None parameters skipped."""
+    from diloco_amd.mirror import module_params
+
+    class Blk(torch.nn.Module):
+        def __init__(self, shared):
+            super().__init__()
+            self.ln = torch.nn.LayerNorm(4)
+            self.fc = torch.nn.Linear(4, 4, bias=False)  # bias registered as None
+            self.shared = shared
+            self.extra = torch.nn.ParameterDict({"b": torch.nn.Parameter(torch.zeros(2)),
+                                                 "a": torch.nn.Parameter(torch.zeros(3))})
+
+    shared = torch.nn.Linear(4, 4)
+    m = torch.nn.Module()
+    m.wte = torch.nn.Embedding(8, 4)
+    m.h = torch.nn.ModuleList([Blk(shared), Blk(shared)])
+    m.again = shared                                  # the same module a third time
+    m.head = torch.nn.Linear(4, 8, bias=False)
+    m.head.weight = m.wte.weight                      # tied
+    m.register_parameter("top", torch.nn.Parameter(torch.ones(1)))
+    m.h[1].register_module("gone", None)
+    got, exp = module_params(m), list(m.parameters())
+    assert len(got) == len(exp)
+    assert all(a is b for a, b in zip(got, exp))
