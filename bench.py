@@ -981,7 +981,7 @@ def dropin_rate(spec, dev, ws, rank, steps, placement="host", write_back="sync",
     return res
 
 
-def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32"):
+def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None):
     """The outer step through the reference's own call surface, src/train.py:263-269 --
     compute_pseudo_gradient -> TrainingComm.sync_gradients -> outer_optimizer.step() ->
     sync_inner_model -- on the device-resident fused outer model (get_outer_model(...,
@@ -990,7 +990,8 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32"):
     while step k's kernels run). N = 1: one dl_delta_pack_sgd per step; N > 1: per bucket
     dl_delta_pack -> RCCL all_reduce, then dl_unpack_sgd (/n, SGD, inner write). wire="bf16":
     BASELINE config #5 behind the same calls (the pack casts to bf16, RCCL sums bf16, the SGD
-    pass reads the wire)."""
+    pass reads the wire). bucket_elems: the DP exchange's bucket size (the
+    DILOCO_OUTER_BUCKET_ELEMS knob; default 64 Mi elements)."""
     from types import SimpleNamespace
 
     from diloco_amd.comm import TrainingComm
@@ -1007,7 +1008,17 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32"):
     inner = torch.nn.Module()
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
-    outer = get_outer_model(inner, "device", fused=True, wire=wire)
+    knob, prev = "DILOCO_OUTER_BUCKET_ELEMS", os.environ.get("DILOCO_OUTER_BUCKET_ELEMS")
+    if bucket_elems is not None:
+        os.environ[knob] = str(int(bucket_elems))
+    try:
+        outer = get_outer_model(inner, "device", fused=True, wire=wire)
+    finally:
+        if bucket_elems is not None:
+            if prev is None:
+                os.environ.pop(knob, None)
+            else:
+                os.environ[knob] = prev
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     # inner = θ_0 + this rank's noise (H inner steps' stand-in); later steps see inner = θ
@@ -1725,6 +1736,12 @@ def main():
             # bucket size for the xGMI pipeline: 64 MiB buckets (more overlap, more calls)
             leg(f"{spec.name}_bucket64MiB", run_tree, spec, dev, ws, rank, a.steps, a.warmup,
                 wire, 16 << 20, False, False)
+            # the same for the headline (the reference's calls on the fused device outer model):
+            # eight 64 MiB buckets instead of two 256 MiB ones, i.e. a shorter exposed pack of the
+            # first bucket and SGD pass of the last against four times the RCCL calls
+            if wire == torch.float32:
+                leg(f"{spec.name}_dropin_bucket64MiB", run_dropin, spec, dev, ws, rank, a.steps,
+                    a.warmup, "f32", 16 << 20, brief=False)
             # the ordered sharded step: all_to_all + rank-order reduce (deterministic, same bus)
             leg(f"{spec.name}_a2a", run_tree, spec, dev, ws, rank, a.steps, a.warmup, wire, cap,
                 False, False, True, "a2a")
