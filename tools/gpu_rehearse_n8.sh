@@ -7,6 +7,11 @@ R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
 TAG=${TAG:-default}
 t0=$(date +%s)
+# a long gloo leg logs nothing for minutes: a heartbeat file keeps gpurun's silence guard
+# from taking the run for hung (the rank processes write their progress to the .err file)
+( while sleep 45; do echo "$(( $(date +%s) - t0 )) s" >> gpurun_out/heartbeat_n8_$TAG.txt; done ) &
+hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
 DILOCO_BENCH_BACKEND=gloo timeout -k 10 ${LIMIT:-600} python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
   --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 $ARGS \
   > gpurun_out/bench_n8_gloo_$TAG.json 2> gpurun_out/bench_n8_gloo_$TAG.err || { echo n8 rehearsal failed; tail -40 gpurun_out/bench_n8_gloo_$TAG.err; exit 1; }
