@@ -142,8 +142,10 @@ class RecvThread:
 # product). "gloo" exists for multi-process tests that share one GPU (RCCL refuses two ranks
 # on one device); the kernels are the same HIP kernels either way.
 DP_BACKEND = os.environ.get("DILOCO_DP_BACKEND", "nccl")
-# The device-gradient average's exchange (gradsync.GradSync): "rccl" = all_reduce; "a2a" =
-# all_to_all + rank-order average + all_gather (deterministic, bit-exact vs the oracle at any n)
+# The DP average's exchange: "rccl" = RCCL's own order (the device-gradient GradSync's
+# all_reduce; the outer model's exchange as get_outer_model chose it); "a2a" = all_to_all +
+# rank-order average + all_gather (deterministic, bit-exact vs the oracle at any n) for the
+# device gradients AND for the outer model's mirror (both placements)
 DP_EXCHANGE = os.environ.get("DILOCO_DP_EXCHANGE", "rccl")
 
 
@@ -180,7 +182,8 @@ class DPSync:
         if m is not None:
             # an outer model whose steps run on the GPU (host placement after a device
             # compute_pseudo_gradient, or placement="device"): its packed mirror reduces
-            m.all_reduce(self.dp_group(m.device), num_peers)
+            # DILOCO_DP_EXCHANGE=a2a: the rank-order (deterministic) exchange here too
+            m.all_reduce(self.dp_group(m.device), num_peers, ordered=DP_EXCHANGE == "a2a")
             return
         from .mirror import module_params
         from .utils import device_path

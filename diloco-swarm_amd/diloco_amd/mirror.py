@@ -29,6 +29,7 @@ device copy is newer is an error, not a silent overwrite.
 """
 from __future__ import annotations
 
+import warnings
 import weakref
 from collections import OrderedDict
 from operator import is_
@@ -56,6 +57,50 @@ def _check_host_params(params: Sequence[torch.Tensor]) -> None:
 
 WRITE_BACKS = ("sync", "deferred")
 OUTER_WIRES = ("f32", "bf16")
+# The DP exchange behind sync_gradients for the device outer model at N > 1:
+#   "sharded"     per bucket RCCL reduce_scatter -> Nesterov SGD on this rank's 1/n of θ and
+#                 the momentum -> RCCL all_gather of θ (20 + 20/n B/param of HBM)
+#   "replicated"  per bucket RCCL all_reduce -> the SGD pass on the whole tree on every rank
+#   "a2a"         "sharded" with an all_to_all + rank-order sum (bit-exact at every n)
+OUTER_EXCHANGES = ("sharded", "replicated", "a2a")
+
+
+def _none():
+    return None
+
+
+def ordered_average(k, tree, wire: torch.Tensor, recv: torch.Tensor, group, n: int,
+                    rank: int) -> None:
+    """wire <- the rank-order average of every peer's wire, bucket by bucket (the ordered
+    form of src/comm.py:120-123, DILOCO_DP_EXCHANGE=a2a): all_to_all hands this rank every
+    peer's copy of its 1/n, dl_shard_reduce_avg sums them in rank order and divides into this
+    rank's slice of the wire, an in-place all_gather returns the other slices. `recv`: a
+    landing buffer the wire's size."""
+    for lo, hi in tree.bucket_ranges:
+        s = (hi - lo) // n
+        dist.all_to_all_single(recv[lo:hi], wire[lo:hi], group=group)
+        k.shard_reduce_avg(recv[lo:hi], n, wire[lo + rank * s:lo + (rank + 1) * s])
+        dist.all_gather_into_tensor(wire[lo:hi], wire[lo + rank * s:lo + (rank + 1) * s],
+                                    group=group)
+
+
+def dp_bucket_align() -> int:
+    """Bucket alignment of an outer model's packed tree: 64 elements times the job's world
+    size, so that any DP group -- its size divides the world size, src/world.py:96-97 -- splits
+    every bucket into equal 256-B-aligned slices. 64 at one process."""
+    if dist.is_available() and dist.is_initialized():
+        ws = dist.get_world_size()
+    else:
+        import os
+
+        ws = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    return _lib.ALIGN_ELEMS * max(1, ws)
+
+
+def shardable(tree, n: int) -> bool:
+    """Every bucket splits into n equal slices of whole 16-B vectors (the tree was planned
+    with buckets aligned to 64 elements times a multiple of n)."""
+    return all((hi - lo) % n == 0 and ((hi - lo) // n) % 4 == 0 for lo, hi in tree.bucket_ranges)
 
 
 class HostOuterMirror:
@@ -70,7 +115,7 @@ class HostOuterMirror:
         self.k = kernels or default_kernels()
         self.device = torch.device(device)
         self.numels = [p.numel() for p in self.params]
-        self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems)
+        self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems, dp_bucket_align())
         self.offs = [int(o) for o in self.tree.seg_off[:-1]]
         total = self.tree.total
         pin = self.device.type == "cuda"
@@ -224,10 +269,19 @@ class HostOuterMirror:
         self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
         self._grads_to_host()
 
-    def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
-        """grad = Σ_peers grad / n (src/comm.py:120-123): RCCL on d_wire, /n in HBM."""
+    def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int,
+                   ordered: bool = False) -> None:
+        """grad = Σ_peers grad / n (src/comm.py:120-123): RCCL on d_wire, /n in HBM.
+        ordered: the rank-order average (all_to_all + dl_shard_reduce_avg + all_gather;
+        DILOCO_DP_EXCHANGE=a2a), when every bucket splits into num_peers slices."""
         self._settle()
         self.grads_to_device(zero_fill_missing=True)
+        if ordered and shardable(self.tree, num_peers):
+            recv = torch.empty_like(self.d_wire)
+            ordered_average(self.k, self.tree, self.d_wire, recv, group, num_peers,
+                            dist.get_rank(group))
+            self._grads_to_host()
+            return
 
         def view(b):
             lo, hi = self.tree.bucket_ranges[b]
@@ -303,6 +357,12 @@ class HostOuterMirror:
     def close(self) -> None:
         self.flush()
         self.tree.close()
+
+    def __deepcopy__(self, memo):  # a copied outer model starts without a mirror
+        return None
+
+    def __reduce_ex__(self, proto):  # ... and so does a pickled one
+        return (_none, ())
 
 
 
@@ -404,6 +464,78 @@ class OuterParameter(torch.nn.Parameter):
     def __reduce_ex__(self, proto):  # pickles as a plain Parameter (the mirror stays behind)
         return (torch._utils._rebuild_parameter, (self.data, self.requires_grad, OrderedDict()))
 
+    def __deepcopy__(self, memo):  # ... and deep-copies as one (a clone of the values)
+        if id(self) in memo:
+            return memo[id(self)]
+        out = torch.nn.Parameter(_DATA.__get__(self).clone(), self.requires_grad)
+        memo[id(self)] = out
+        return out
+
+
+# Tensor functions that read metadata only: they never make a sharded momentum gather
+_META = frozenset([
+    torch.Tensor.data_ptr, torch.Tensor.size, torch.Tensor.dim, torch.Tensor.numel,
+    torch.Tensor.stride, torch.Tensor.storage_offset, torch.Tensor.is_contiguous,
+    torch.Tensor.element_size, torch.Tensor.nelement, torch.Tensor.ndimension,
+    torch.Tensor.shape.__get__, torch.Tensor.dtype.__get__, torch.Tensor.device.__get__,
+    torch.Tensor.ndim.__get__, torch.Tensor._version.__get__, torch.Tensor.is_cuda.__get__,
+    torch.Tensor.layout.__get__, torch.Tensor.requires_grad.__get__,
+    torch.Tensor.is_leaf.__get__, torch.Tensor.grad.__get__, torch.Tensor.__len__,
+])
+
+
+def _gather_momentum_of(args, kwargs) -> None:
+    seen = set()
+
+    def visit(x):
+        if isinstance(x, MomentumBuffer):
+            r = x.__dict__.get("_dl_mirror")
+            m = r() if r is not None else None
+            if m is not None and id(m) not in seen:
+                seen.add(id(m))
+                m.gather_momentum()
+        elif isinstance(x, (list, tuple)):
+            for y in x:
+                visit(y)
+
+    visit(args)
+    if kwargs:
+        visit(tuple(kwargs.values()))
+
+
+class MomentumBuffer(torch.Tensor):
+    """`outer_optimizer.state[p]["momentum_buffer"]` of a fused device outer model (a view of
+    its packed momentum arena). Under the sharded exchange every rank's SGD pass updates only
+    its own 1/n of the momentum; the rest of the arena is gathered from the peers
+    the first time anything reads the values -- any torch function on a buffer other than a
+    metadata query, its pickling and its deep copy -- so every value a caller observes is the
+    reference's full, replicated momentum (src/utils.py:62-63, torch SGD's state). That gather
+    is an all_gather over the DP group: like reading .grad under the sharded exchange, it is a
+    collective, made by every rank of the group (as torch.save of the optimizer state in the
+    reference's multi-rank runs is). Results of operations are plain tensors."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        if func not in _META:
+            _gather_momentum_of(args, kwargs)
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **(kwargs or {}))
+
+    def _plain(self) -> torch.Tensor:
+        _gather_momentum_of((self,), None)
+        with torch._C.DisableTorchFunctionSubclass():
+            return self.detach().clone()
+
+    def __deepcopy__(self, memo):
+        if id(self) in memo:
+            return memo[id(self)]
+        out = self._plain()
+        memo[id(self)] = out
+        return out
+
+    def __reduce_ex__(self, proto):  # pickles as a plain tensor of the gathered values
+        return self._plain().__reduce_ex__(proto)
+
 
 class DeviceOuterMirror:
     """Device-resident outer model: the outer parameters, their .grad and
@@ -438,9 +570,12 @@ class DeviceOuterMirror:
 
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
                  bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = False,
-                 wire: str = "f32"):
+                 wire: str = "f32", exchange: str = "sharded"):
         if wire not in OUTER_WIRES:
             raise ValueError(f"wire {wire!r}: one of {OUTER_WIRES}")
+        if exchange not in OUTER_EXCHANGES:
+            raise ValueError(f"exchange {exchange!r}: one of {OUTER_EXCHANGES}")
+        self.exchange = exchange
         self.params: List[torch.nn.Parameter] = module_params(outer_model)
         if not self.params:
             raise ValueError("outer model has no parameters")
@@ -453,7 +588,7 @@ class DeviceOuterMirror:
                 raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
         self.fused = fused
         self.numels = [p.numel() for p in self.params]
-        self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems)
+        self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems, dp_bucket_align())
         self.offs = [int(o) for o in self.tree.seg_off[:-1]]
         z = dict(dtype=torch.float32, device=self.device)
         self.d_theta = torch.zeros(self.tree.total, **z)
@@ -487,6 +622,29 @@ class DeviceOuterMirror:
         self._target = None  # (inner params, ptrs, versions) of the last compute_pseudo_gradient
         self._synced = None  # (inner params, ptrs, versions, θ versions): inner holds θ
         self._mom_src: Optional[List[torch.Tensor]] = None  # the buffers the last step returned
+        # sharded exchange state (fused, N > 1): the wire after the collectives ("sharded":
+        # this rank's slice of each bucket holds the Σ -- or, after an a2a reduce, the average
+        # -- the rest this rank's own deltas; "a2a": the n slices are still in d_recv), the DP
+        # group, its size and this rank's index in it; the momentum arena holds this rank's
+        # slices only (the rest gathered on first read, MomentumBuffer)
+        self._xmode: Optional[str] = None
+        self._xgroup, self._xn, self._xrank = None, 1, 0
+        self._mom_stale = False
+        self._mom_shard = None  # (group, n, rank) of the steps that left it sharded
+        self.d_recv: Optional[torch.Tensor] = None  # a2a landing arena (the wire's size)
+        self._warned = False
+
+    def _momentum_buffer(self, view: torch.Tensor) -> "MomentumBuffer":
+        t = view.as_subclass(MomentumBuffer)
+        t.__dict__["_dl_mirror"] = weakref.ref(self)
+        return t
+
+    def __deepcopy__(self, memo):  # a copied outer model starts without a mirror
+        return None
+
+    def __reduce_ex__(self, proto):  # ... and so does a pickled one
+        return (_none, ())
+
     def _install_outer_parameters(self, model: torch.nn.Module) -> None:
         """Fused mode: every parameter of the outer model becomes an OuterParameter created
         over its view of the θ arena (shared parameters stay shared). A tensor made from a view
@@ -589,7 +747,95 @@ class DeviceOuterMirror:
     @property
     def pending(self) -> bool:
         return (self._delta is not None or self._div != 1 or self._sum16
-                or self._works is not None)
+                or self._works is not None or self._xmode is not None)
+
+    # ---- the sharded exchange (fused, N > 1) ---------------------------------------------
+    def _own(self, b: int, n: int, rank: int):
+        """[a, e): this rank's slice of bucket b when the bucket is split n ways."""
+        lo, hi = self.tree.bucket_ranges[b]
+        s = (hi - lo) // n
+        return lo + rank * s, lo + (rank + 1) * s
+
+    def _exchange_mode(self, n: int, ordered: bool) -> str:
+        mode = "a2a" if ordered else self.exchange
+        if self.wire == "bf16":
+            if ordered and not self._warned:
+                self._warned = True
+                warnings.warn("the bf16 outer wire reduces with RCCL's bf16 all_reduce; "
+                              "DILOCO_DP_EXCHANGE=a2a applies to the fp32 wire only")
+            return "replicated"
+        if mode == "sharded" and not self.fused:
+            return "replicated"  # eager: .grad holds the full average right after the call
+        if mode != "replicated" and not shardable(self.tree, n):
+            if not self._warned:
+                self._warned = True
+                warnings.warn(f"outer-model buckets do not split into {n} equal slices (the "
+                              "tree was planned for another world size): replicated exchange")
+            return "replicated"
+        return mode
+
+    def _gather_wire(self) -> None:
+        """The pending sharded wire -> every bucket's full Σ (or average) on every rank: the
+        a2a slices reduced in rank order, then an in-place all_gather per bucket."""
+        mode, self._xmode = self._xmode, None
+        n, r, g = self._xn, self._xrank, self._xgroup
+        for b in range(self.tree.n_buckets):
+            lo, hi = self.tree.bucket_ranges[b]
+            a, e = self._own(b, n, r)
+            if mode == "a2a":
+                self.k.shard_reduce_avg(self.d_recv[lo:hi], n, self.d_wire[a:e])
+            dist.all_gather_into_tensor(self.d_wire[lo:hi], self.d_wire[a:e], group=g)
+
+    def gather_momentum(self) -> None:
+        """The momentum arena whole again after sharded steps (each rank updated its own
+        slices): an in-place all_gather per bucket over the DP group of those steps."""
+        if not self._mom_stale:
+            return
+        self._mom_stale = False
+        g, n, r = self._mom_shard
+        for b in range(self.tree.n_buckets):
+            lo, hi = self.tree.bucket_ranges[b]
+            a, e = self._own(b, n, r)
+            dist.all_gather_into_tensor(self.d_mom[lo:hi], self.d_mom[a:e], group=g)
+
+    def _sharded_sgd(self, mom, lr, momentum, nesterov, first, target) -> None:
+        """Per bucket: wait for its reduce_scatter (a2a: all_to_all, then dl_shard_reduce_avg
+        into this rank's slice of the wire), dl_shard_sgd on this rank's slice of θ and the
+        momentum (/n, torch's Nesterov arithmetic), an in-place RCCL all_gather of θ, and --
+        one bucket behind -- dl_scatter of the gathered θ into the inner params."""
+        works, self._works = self._works, None
+        mode, n, r, g = self._xmode, self._xn, self._xrank, self._xgroup
+        write = target is not None
+        if write:
+            self.k.bind(self.tree, SLOT_INNER, target[0], self.device, key=tuple(target[1]))
+        nb = self.tree.n_buckets
+        ags = [None] * nb
+        for b in range(nb):
+            if works is not None:
+                works[b].wait()
+            lo, hi = self.tree.bucket_ranges[b]
+            a, e = self._own(b, n, r)
+            if mode == "a2a":
+                self.k.shard_reduce_avg(self.d_recv[lo:hi], n, self.d_wire[a:e])
+            self.k.shard_sgd(self.d_wire[a:e], 1 if mode == "a2a" else n, self.d_theta[a:e],
+                             None if mom is None else mom[a:e], lr, momentum, nesterov, first)
+            ags[b] = dist.all_gather_into_tensor(self.d_theta[lo:hi], self.d_theta[a:e],
+                                                 group=g, async_op=True)
+            if b >= 1:
+                ags[b - 1].wait()
+                if write:
+                    self.k.scatter(self.tree, b - 1, self.d_theta, SLOT_INNER)
+        ags[nb - 1].wait()
+        if write:
+            self.k.scatter(self.tree, nb - 1, self.d_theta, SLOT_INNER)
+        # the wire keeps this rank's slices (Σ; after an a2a reduce the average) for a later
+        # .grad read; the momentum holds this rank's slices only
+        self._xmode = "sharded"
+        if mode == "a2a":
+            self._div = 1
+        if mom is not None:
+            self._mom_stale = True
+            self._mom_shard = (g, n, r)
 
     def _take_delta(self, tver_now=None) -> List[torch.Tensor]:
         """The pending delta's inner params, checked unchanged since compute_pseudo_gradient
@@ -620,6 +866,8 @@ class DeviceOuterMirror:
         if self._delta is not None:
             self._take_delta()
             self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
+        if self._xmode is not None:  # sharded: a collective over the DP group (see class doc)
+            self._gather_wire()
         if self._sum16:  # bf16 wire: the decoded average (/n in fp32) into .grad's arena
             div, self._div, self._sum16 = self._div, 1, False
             self.k.unpack_avg(self.tree, ALL, self.d_wire16, div, -1, self.d_wire)
@@ -629,9 +877,11 @@ class DeviceOuterMirror:
 
     def flush(self) -> None:
         """No host copy to write back (torch copies to the host on demand); completes the
-        deferred .grad work."""
+        deferred .grad work and gathers a sharded momentum (collectives under the sharded
+        exchange)."""
         if self.fused:
             self.settle_grads()
+            self.gather_momentum()
 
     def _grad_views(self) -> None:
         if not self.fused or self.grads_touched:
@@ -651,6 +901,7 @@ class DeviceOuterMirror:
         self.k.bind(self.tree, SLOT_INNER, inner, self.device, key=tuple(iptrs))
         self._div = 1  # the wire is overwritten: a /n still pending is moot
         self._sum16 = False
+        self._xmode = None
         if self.fused:
             ivers = _vers(inner)
             self._delta = (inner, iptrs, ivers, tver)
@@ -659,10 +910,16 @@ class DeviceOuterMirror:
             self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
         self._grad_views()
 
-    def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int) -> None:
-        """grad = Σ_peers grad / n (src/comm.py:120-123), in place on the packed .grad."""
+    def all_reduce(self, group: Optional[dist.ProcessGroup], num_peers: int,
+                   ordered: bool = False) -> None:
+        """grad = Σ_peers grad / n (src/comm.py:120-123), in place on the packed .grad.
+        ordered (DILOCO_DP_EXCHANGE=a2a): the rank-order sum, bit-exact at every n."""
+        mode = self._exchange_mode(num_peers, ordered)
         if self.wire == "bf16":
             self._all_reduce_bf16(group, num_peers)
+            return
+        if mode != "replicated":
+            self._all_reduce_sharded(group, num_peers, mode)
             return
         pack = None
         if self._delta is not None:  # fused: each bucket packed just before its collective
@@ -728,6 +985,47 @@ class DeviceOuterMirror:
             lambda b: self.k.unpack_avg(self.tree, b, w16, num_peers, -1, self.d_wire),
         )
 
+    def _all_reduce_sharded(self, group, n: int, mode: str) -> None:
+        """Fused: per bucket pack (the pending delta) then an asynchronous in-place RCCL
+        reduce_scatter into this rank's slice of the bucket (mode "a2a": an all_to_all of the
+        bucket into d_recv); none waited for here -- OuterSGD.step waits bucket by bucket, a
+        .grad read gathers the whole average first. Eager (mode "a2a" only): the rank-order
+        average of every bucket into .grad at once."""
+        pack = None
+        if self._delta is not None:
+            self._take_delta()
+            self._relay_theta()
+            self._grad_views()
+
+            def pack(b):
+                self.k.delta_pack(self.tree, b, SLOT_INNER, self.d_theta, self.d_wire)
+        else:
+            if self.pending:
+                self.settle_grads()  # a second sync_gradients reduces the averages
+            self._relay_grads(zero_fill_missing=True)
+        rank = dist.get_rank(group)
+        if mode == "a2a" and self.d_recv is None:
+            self.d_recv = torch.empty_like(self.d_wire)
+        if not self.fused:
+            ordered_average(self.k, self.tree, self.d_wire, self.d_recv, group, n, rank)
+            return
+        works = []
+        for b in range(self.tree.n_buckets):
+            if pack is not None:
+                pack(b)
+            lo, hi = self.tree.bucket_ranges[b]
+            a, e = self._own(b, n, rank)
+            if mode == "a2a":
+                works.append(dist.all_to_all_single(self.d_recv[lo:hi], self.d_wire[lo:hi],
+                                                    group=group, async_op=True))
+            else:
+                works.append(dist.reduce_scatter_tensor(self.d_wire[a:e], self.d_wire[lo:hi],
+                                                        op=dist.ReduceOp.SUM, group=group,
+                                                        async_op=True))
+        self._works = works
+        self._xmode, self._xgroup, self._xn, self._xrank = mode, group, n, rank
+        self._div = n if mode == "sharded" else 1
+
     def _launch_reductions(self, pack, view, group) -> None:
         """Fused N > 1: pack(b) then an asynchronous all_reduce(SUM) of bucket b, for every
         bucket, none waited for here (OuterSGD.step waits bucket by bucket, anything that reads
@@ -754,8 +1052,10 @@ class DeviceOuterMirror:
         if momentum != 0:
             if self.d_mom is None:
                 self.d_mom = torch.zeros_like(self.d_theta)
-                self._views["mom"] = self._make_views(self.d_mom)
-                self._ptrs["mom"] = [v.data_ptr() for v in self._views["mom"]]
+                plain = self._make_views(self.d_mom)
+                self._views["mom_plain"] = plain
+                self._views["mom"] = [self._momentum_buffer(v) for v in plain]
+                self._ptrs["mom"] = [v.data_ptr() for v in plain]
             bufs = self._views["mom"]
             src = self._mom_src
             if not (src is not None and len(host_bufs) == len(src)
@@ -765,14 +1065,23 @@ class DeviceOuterMirror:
                     raise RuntimeError("momentum buffers exist for some outer parameters only")
                 first = not any(have)
                 if not first:
+                    copied = 0
                     with torch.no_grad():
-                        for b, v, e in zip(host_bufs, bufs, self._ptrs["mom"]):
-                            if b.data_ptr() != e:
+                        for b, v, e in zip(host_bufs, self._views["mom_plain"],
+                                           self._ptrs["mom"]):
+                            if _DATA_PTR(b) != e:
                                 v.copy_(b)  # e.g. a state_dict loaded into the optimizer
+                                copied += 1
+                    if copied == len(host_bufs):
+                        self._mom_stale = False  # every slice written from the caller's
             else:
                 first = False  # the buffers this mirror returned last step
             self._mom_src = bufs
         mom = self.d_mom if momentum != 0 else None
+        sharded = delta is None and self._xmode is not None
+        if (mom is not None and self._mom_stale and not first
+                and not (sharded and self._mom_shard == (self._xgroup, self._xn, self._xrank))):
+            self.gather_momentum()  # a whole-tree update needs every slice of the momentum
         # the inner params of the last compute_pseudo_gradient take θ_new in the same pass
         # (fused mode). The record of that write keeps their addresses and versions from then:
         # if they moved or were written since, sync_inner_model sees it and scatters again
@@ -781,7 +1090,11 @@ class DeviceOuterMirror:
         if delta is not None:  # one peer: the delta never leaves registers
             self.k.delta_pack_sgd(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire, mom,
                                   lr, momentum, nesterov, first)
+            self._mom_stale = False
+        elif sharded:  # N > 1, sharded exchange: this rank's 1/n, then all_gather(θ)
+            self._sharded_sgd(mom, lr, momentum, nesterov, first, target)
         else:
+            self._mom_stale = False
             if write:
                 self.k.bind(self.tree, SLOT_INNER, target[0], self.device, key=tuple(target[1]))
             # a pending /n stays pending: the wire keeps the Σ, .grad settles it when read

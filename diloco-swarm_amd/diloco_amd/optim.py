@@ -5,16 +5,17 @@ runs use Nesterov, configs/optimizer/nesterov.toml, lr 0.7 at experiments/experi
 returns an `OuterSGD`. It IS a torch.optim.SGD (param_groups, state_dict, LR schedulers work
 unchanged) whose step() runs `_single_tensor_sgd`'s arithmetic for the whole tree in one
 dl_unpack_sgd launch on the device mirror of the outer model (mirror.HostOuterMirror), then
-writes θ and the momentum buffers back to the host tensors the optimizer owns.
+writes θ and the momentum buffers back to the host tensors the optimizer owns; on the device
+outer model (mirror.DeviceOuterMirror) its state's momentum buffers are views of the packed
+HBM momentum (mirror.MomentumBuffer).
 """
 from __future__ import annotations
 
-from itertools import chain
+import inspect
 from operator import is_, methodcaller
 
 import torch
 from torch.optim import SGD
-from torch.optim import optimizer as _optim
 
 from .mirror import HostOuterMirror
 
@@ -39,35 +40,11 @@ class OuterSGD(SGD):
         flush_outer_model(self._model)
         return super().state_dict()
 
+    @torch.no_grad()
     def step(self, closure=None):
-        """torch.optim.Optimizer's step wrapper (profile_hook_step) restated: the pre / post
-        hooks (global and per-optimizer) run as there, but the record_function annotation is
-        made only while the autograd profiler runs -- it is a quarter of the host time of an
-        outer step otherwise (the kernel itself is one launch)."""
-        args, kwargs = (self,), ({} if closure is None else {"closure": closure})
-        for pre in chain(_optim._global_optimizer_pre_hooks.values(),
-                         self._optimizer_step_pre_hooks.values()):
-            res = pre(self, args, kwargs)
-            if res is not None:
-                if isinstance(res, tuple) and len(res) == 2:
-                    args, kwargs = res
-                else:
-                    raise RuntimeError(f"{self.step} must return None or a tuple of "
-                                       f"(new_args, new_kwargs), but got {res}.")
-        if torch.autograd._profiler_enabled():
-            with torch.autograd.profiler.record_function(f"Optimizer.step#{type(self).__name__}.step"):
-                out = self._step(*args[1:], **kwargs)
-        else:
-            out = self._step(*args[1:], **kwargs)
-        self._optimizer_step_code()
-        for post in chain(self._optimizer_step_post_hooks.values(),
-                          _optim._global_optimizer_post_hooks.values()):
-            post(self, args, kwargs)
-        return out
-
-    step.hooked = True  # torch.optim.Optimizer._patch_step_function: already wrapped (above)
-
-    def _step(self, closure=None):
+        """One outer SGD step (src/train.py:267). torch.optim.Optimizer wraps it as it wraps
+        every optimizer's step (its profiler annotation, the global and per-optimizer pre /
+        post hooks), so hooks and LR schedulers see an ordinary SGD."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -86,9 +63,9 @@ class OuterSGD(SGD):
             from .utils import device_path
         if mirror is None and not device_path(g["params"][0]):
             # host tensors never stepped on the GPU (the reference's --device cpu runs):
-            # torch.optim.SGD itself, as src/utils.py:62-63 builds it (its own no_grad)
-            fn = SGD.step  # hook-wrapped once a plain SGD exists: the hooks ran above
-            (fn.__wrapped__ if getattr(fn, "hooked", False) else fn)(self)
+            # torch.optim.SGD's own step body, as src/utils.py:62-63 builds it -- unwrapped,
+            # since this call already runs inside the hook wrapper (no_grad is ours)
+            inspect.unwrap(SGD.step)(self)
             return loss
         if mirror is None:
             mirror = self._mirror()

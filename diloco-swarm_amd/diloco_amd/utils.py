@@ -51,8 +51,8 @@ import torch.nn as nn
 from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
-from .mirror import (OUTER_WIRES, WRITE_BACKS, DeviceOuterMirror, HostOuterMirror,
-                     module_params)
+from .mirror import (OUTER_EXCHANGES, OUTER_WIRES, WRITE_BACKS, DeviceOuterMirror,
+                     HostOuterMirror, module_params)
 from .optim import OuterSGD
 from .plan import DEFAULT_BUCKET_CAP_ELEMS
 
@@ -62,7 +62,24 @@ _PLACEMENT = "_diloco_placement"
 _WRITE_BACK = "_diloco_write_back"
 _FUSED = "_diloco_fused"
 _WIRE = "_diloco_wire"
+_EXCHANGE = "_diloco_exchange"
 PLACEMENTS = ("host", "device")
+_TRUE = ("1", "true", "on", "yes")
+_FALSE = ("0", "false", "off", "no")
+
+
+def env_flag(name: str, default: bool) -> bool:
+    """A boolean knob from the environment: 1/0, true/false, on/off, yes/no (any case);
+    anything else raises instead of silently meaning "on"."""
+    v = os.environ.get(name)
+    if v is None or v.strip() == "":
+        return default
+    v = v.strip().lower()
+    if v in _TRUE:
+        return True
+    if v in _FALSE:
+        return False
+    raise ValueError(f"{name}={os.environ[name]!r}: one of {_TRUE + _FALSE}")
 
 
 def device_path(t: torch.Tensor) -> bool:
@@ -89,7 +106,8 @@ def outer_mirror(outer_model: nn.Module, device=None):
             cap = int(os.environ.get("DILOCO_OUTER_BUCKET_ELEMS", DEFAULT_BUCKET_CAP_ELEMS))
             m = DeviceOuterMirror(outer_model, p.device, kernels=k, bucket_cap_elems=cap,
                                   fused=getattr(outer_model, _FUSED, False),
-                                  wire=getattr(outer_model, _WIRE, "f32"))
+                                  wire=getattr(outer_model, _WIRE, "f32"),
+                                  exchange=getattr(outer_model, _EXCHANGE, "sharded"))
             object.__setattr__(outer_model, _ATTR, m)
             return m
         if device is None:
@@ -112,13 +130,14 @@ def _inner_device(inner_model: nn.Module) -> torch.device:
 
 
 def get_outer_model(inner_model: nn.Module, placement: str = None,
-                    write_back: str = None, fused: bool = None, wire: str = None) -> nn.Module:
+                    write_back: str = None, fused: bool = None, wire: str = None,
+                    exchange: str = None) -> nn.Module:
     """Initializes the outer model from the inner model (src/utils.py:213-216).
 
     placement "host" (the reference's, default) or "device"; write_back "sync" (default) or
-    "deferred" for the host placement; fused (default on) and wire ("f32" default, "bf16":
-    BASELINE config #5's codec on the DP exchange) for the device placement (see the module
-    docstring)."""
+    "deferred" for the host placement; fused (default on), wire ("f32" default, "bf16":
+    BASELINE config #5's codec on the DP exchange) and exchange ("sharded" default,
+    "replicated", "a2a") for the device placement (see the module docstring)."""
     if placement is None:
         placement = os.environ.get("DILOCO_OUTER_PLACEMENT", "host")
     if placement not in PLACEMENTS:
@@ -128,11 +147,15 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     if write_back not in WRITE_BACKS:
         raise ValueError(f"write_back {write_back!r}: one of {WRITE_BACKS}")
     if fused is None:
-        fused = os.environ.get("DILOCO_OUTER_FUSED", "1") not in ("0", "")
+        fused = env_flag("DILOCO_OUTER_FUSED", True)
     if wire is None:
         wire = os.environ.get("DILOCO_OUTER_WIRE", "f32")
     if wire not in OUTER_WIRES:
         raise ValueError(f"wire {wire!r}: one of {OUTER_WIRES}")
+    if exchange is None:
+        exchange = os.environ.get("DILOCO_OUTER_EXCHANGE", "sharded")
+    if exchange not in OUTER_EXCHANGES:
+        raise ValueError(f"exchange {exchange!r}: one of {OUTER_EXCHANGES}")
     if wire != "f32" and placement != "device":
         raise ValueError("the bf16 outer wire needs placement='device' (the host placement "
                          "keeps the reference's fp32 host tensors end to end)")
@@ -155,6 +178,7 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     object.__setattr__(outer_model, _WRITE_BACK, write_back)
     object.__setattr__(outer_model, _FUSED, bool(fused) and placement == "device")
     object.__setattr__(outer_model, _WIRE, wire)
+    object.__setattr__(outer_model, _EXCHANGE, exchange)
     if placement == "device" and has_params:
         # lay the parameters out in the packed HBM arena now (fused: as OuterParameters);
         # a model without parameters keeps none: the four calls are the reference's empty loops

@@ -43,7 +43,8 @@ def expected_rank_order(n, steps=2, wire="f32"):
     out = {}
     for s in range(1, steps + 1):
         inners = [synth.inner_tree(st.theta, s, r) for r in range(n)]
-        st.step(inners, wire)
+        _, avg = st.step(inners, wire)
+        out[f"avg_s{s}"] = np.concatenate(avg)
         out[f"theta_s{s}"] = np.concatenate(st.theta)
         out[f"buf_s{s}"] = np.concatenate(st.buf)
     return out

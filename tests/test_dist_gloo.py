@@ -73,21 +73,33 @@ def _worker(rank, world, port, mode, num_stages, out):
     rec = {}
     if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_host",
                 "dropin_device_quiet", "dropin_device_eager", "dropin_device_bf16",
-                "dropin_device_bf16_eager", "dropin_device_quiet_buckets"):
-        if mode == "dropin_device_quiet_buckets":  # the exchange in several buckets: the SGD
-            os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # pass waits bucket by bucket
+                "dropin_device_bf16_eager", "dropin_device_quiet_buckets",
+                "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
+                "dropin_device_a2a_dp", "dropin_a2a_dp", "dropin_device_momentum_first",
+                "dropin_device_eager_a2a_dp"):
+        if mode in ("dropin_device_quiet_buckets", "dropin_device_quiet_a2a",
+                    "dropin_device_momentum_first"):  # the exchange in several buckets: the
+            os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # SGD waits bucket by bucket
+        if mode.endswith("_a2a_dp"):  # DILOCO_DP_EXCHANGE=a2a behind sync_gradients
+            import diloco_amd.comm as comm_mod
+
+            comm_mod.DP_EXCHANGE = "a2a"
+        exchange = ("replicated" if mode.endswith("_replicated")
+                    else "a2a" if mode == "dropin_device_quiet_a2a" else None)
         from diloco_amd.utils import flush_outer_model, has_mirror
 
         deferred = mode == "dropin_deferred"
         # quiet: nothing reads the outer model between the four calls (src/train.py:261-269),
         # so the fused device model defers the delta and the /n into its one SGD pass
-        quiet = mode in ("dropin_device_quiet", "dropin_device_bf16", "dropin_device_quiet_buckets")
+        quiet = mode in ("dropin_device_quiet", "dropin_device_bf16", "dropin_device_quiet_buckets",
+                         "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
+                         "dropin_device_a2a_dp", "dropin_device_momentum_first")
         device = mode.startswith("dropin_device")
         inner = _micro_module(theta0, shapes)
         outer = get_outer_model(inner, placement="device" if device else None,
                                 write_back="deferred" if deferred else None,
-                                fused=not mode.endswith("_eager"),
-                                wire="bf16" if "bf16" in mode else None)
+                                fused="_eager" not in mode,
+                                wire="bf16" if "bf16" in mode else None, exchange=exchange)
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
         assert type(opt).__name__ == "OuterSGD"
         from diloco_amd.utils import outer_mirror
@@ -97,8 +109,8 @@ def _worker(rank, world, port, mode, num_stages, out):
             assert type(outer_mirror(outer)).__name__ == (
                 "DeviceOuterMirror" if device else "HostOuterMirror")
             if device:
-                assert outer_mirror(outer).fused == (not mode.endswith("_eager"))
-                if mode.endswith("_buckets"):
+                assert outer_mirror(outer).fused == ("_eager" not in mode)
+                if "DILOCO_OUTER_BUCKET_ELEMS" in os.environ:
                     assert outer_mirror(outer).tree.n_buckets > 2
         comm = TrainingComm(world_, (1, 1, 32), None)
         for s in range(1, MICRO_STEPS + 1):
@@ -126,6 +138,9 @@ def _worker(rank, world, port, mode, num_stages, out):
             elif deferred and len(world_.dp_ranks) > 1:  # the host still has step 1's averages
                 assert host(p.grad for p in outer.parameters()).tobytes() == rec["avg_s1"].tobytes()
             opt.step()
+            if device and quiet and len(world_.dp_ranks) > 1:  # which exchange the step ran
+                m = outer_mirror(outer)
+                rec["sharded_step"] = np.array([m._mom_stale, m._xmode is not None])
             if deferred and s == 1:
                 flush_outer_model(outer)
             if mid:
@@ -135,9 +150,27 @@ def _worker(rank, world, port, mode, num_stages, out):
             if not mid:
                 if deferred:  # quiet: reading .grad itself completes the pending /n
                     flush_outer_model(outer)
+                if mode == "dropin_device_momentum_first":
+                    # the sharded momentum gathered first (through a deepcopy of the state and
+                    # a torch.save round trip), .grad after it
+                    import copy
+                    import io
+
+                    st = copy.deepcopy(dict(opt.state))  # MomentumBuffer.__deepcopy__
+                    assert all(type(v["momentum_buffer"]) is torch.Tensor for v in st.values())
+                    rec[f"buf_s{s}"] = host(v["momentum_buffer"] for v in st.values())
+                    bio = io.BytesIO()
+                    torch.save(opt.state_dict(), bio)
+                    bio.seek(0)
+                    ld = torch.load(bio, weights_only=True)
+                    assert host(ld["state"][i]["momentum_buffer"] for i in range(
+                        len(ld["state"]))).tobytes() == rec[f"buf_s{s}"].tobytes()
                 rec[f"avg_s{s}"] = host(p.grad for p in outer.parameters())
                 rec[f"theta_s{s}"] = host(outer.parameters())
-                rec[f"buf_s{s}"] = host(opt.state[p]["momentum_buffer"] for p in outer.parameters())
+                bufs = host(opt.state[p]["momentum_buffer"] for p in outer.parameters())
+                if mode == "dropin_device_momentum_first":
+                    assert bufs.tobytes() == rec[f"buf_s{s}"].tobytes()
+                rec[f"buf_s{s}"] = bufs
             rec[f"inner_s{s}"] = np.concatenate([p.detach().numpy().reshape(-1) for p in inner.parameters()])
         if mode == "dropin_host":
             assert not has_mirror(outer)  # every call took the reference's host semantics
@@ -289,7 +322,10 @@ def _run(mode, world, num_stages=1):
 
 
 @pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_device_quiet",
-                                  "dropin_device_quiet_buckets",
+                                  "dropin_device_quiet_buckets", "dropin_device_quiet_replicated",
+                                  "dropin_device_quiet_a2a", "dropin_device_a2a_dp",
+                                  "dropin_a2a_dp", "dropin_device_momentum_first",
+                                  "dropin_device_eager_a2a_dp",
                                   "dropin_device_eager", "dropin_deferred", "engine",
                                   "engine_ar", "engine_a2a", "dropin_host"])
 def test_two_peers_match_reference_bit_exact(mode):
@@ -302,16 +338,38 @@ def test_two_peers_match_reference_bit_exact(mode):
             assert rec[f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
             if mode.startswith("dropin"):
                 assert rec[f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
-    if mode.startswith("dropin") and not mode.startswith("dropin_device_quiet"):
+    if mode.startswith("dropin") and "delta_s1" in recs[0]:
         assert recs[0]["delta_s1"].tobytes() == g["delta_s1_r0"].tobytes()
         assert recs[1]["delta_s1"].tobytes() == g["delta_s1_rlast"].tobytes()
+    if "sharded_step" in recs[0]:  # the fused device model's exchange: sharded unless asked
+        want = not mode.endswith("_replicated")
+        assert all(bool(r["sharded_step"].all()) == want for r in recs), mode
+
+
+@pytest.mark.parametrize("mode", ["dropin_device_quiet_a2a", "dropin_device_a2a_dp",
+                                  "dropin_a2a_dp", "dropin_device_eager_a2a_dp"])
+@pytest.mark.parametrize("world", [4, 8])
+def test_dropin_ordered_exchange_is_bit_exact_at_any_n(mode, world):
+    """The outer model's ordered exchange (get_outer_model(..., exchange="a2a"), or
+    DILOCO_DP_EXCHANGE=a2a behind TrainingComm.sync_gradients, host and device placements,
+    fused and eager): every replica's .grad, θ, momentum and inner params bit-identical to the
+    oracle's rank-order restatement at 4 and 8 peers (the reduce-scatter / all_reduce order
+    is the transport's)."""
+    exp = expected_rank_order(world)
+    for rec in _run(mode, world):
+        for s in (1, 2):
+            for k in ("theta", "buf", "avg"):
+                assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (mode, k, s)
+            assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), (mode, s)
 
 
 @pytest.mark.parametrize("mode,world", [("dropin", 4), ("engine", 4), ("engine_ar", 4),
                                         ("dropin", 8), ("engine", 8), ("dropin_host", 4),
                                         ("dropin_device_quiet", 4),
                                         ("dropin_device_quiet_buckets", 4),
-                                        ("dropin_device_quiet_buckets", 8)])
+                                        ("dropin_device_quiet_buckets", 8),
+                                        ("dropin_device_momentum_first", 8),
+                                        ("dropin_device_quiet_replicated", 4)])
 def test_four_and_eight_peers_match_reference_normwise(mode, world):
     """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""
     from diloco_amd.trees import get_tree
