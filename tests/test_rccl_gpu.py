@@ -402,3 +402,75 @@ def test_rccl_p2p_payload_leg_carries_serialized_frames():
         for i in range(2):
             assert rec[f"{name}_{i}_meta"].tolist() == [3, 40 + i]
             assert rec[f"{name}_{i}_bytes_equal"][0] and rec[f"{name}_{i}_payload"][0], (name, i)
+
+
+def _worker_mirror(rank, port, out):
+    """The fused device outer model's exchanges over a real one-rank RCCL communicator
+    (ADVICE r03): DeviceOuterMirror.all_reduce(rccl_group, 1) called directly with buckets of
+    4096 elements (several per tree), so every bucket's collective is still in flight when the
+    call returns and OuterSGD.step waits on the held Work handles bucket by bucket -- the
+    replicated all_reduce, the sharded reduce_scatter -> shard SGD -> all_gather(θ) -> scatter,
+    and the ordered all_to_all form -- then sync_inner_model; θ, the momentum buffers (gathered
+    on read), the inner params and .grad recorded after each of 2 outer steps."""
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from datetime import timedelta
+    from types import SimpleNamespace
+
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      DILOCO_OUTER_BUCKET_ELEMS="4096")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", device_id=dev, timeout=timedelta(seconds=120))
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  outer_mirror, sync_inner_model)
+
+    group = dist.new_group([0], backend="nccl")
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    rec = {}
+    for ex in ("replicated", "sharded", "a2a"):
+        inner = torch.nn.Module()
+        inner.ps = torch.nn.ParameterList([torch.nn.Parameter(t.view(s)) for t, s in zip(
+            synth.outer_tree_device(spec, dev), shapes)])
+        outer = get_outer_model(inner, "device", fused=True, exchange=ex)
+        opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9,
+                                                   nesterov=True))
+        m = outer_mirror(outer)
+        rec[f"{ex}_buckets"] = np.array([m.tree.n_buckets])
+        for s in (1, 2):
+            synth.inner_tree_device([p.data.view(-1) for p in outer.parameters()], s, 0,
+                                    out=[p.data.view(-1) for p in inner.parameters()])
+            compute_pseudo_gradient(inner, outer)
+            m.all_reduce(group, 1)  # TrainingComm.sync_gradients at n > 1 calls exactly this
+            rec[f"{ex}_inflight_s{s}"] = np.array([m._works is not None])
+            opt.step()
+            sync_inner_model(outer, inner)
+            rec[f"{ex}_sharded_s{s}"] = np.array([m._mom_stale])
+            rec[f"{ex}_theta_s{s}"] = _flat(outer.parameters())
+            rec[f"{ex}_buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"]
+                                          for p in outer.parameters())
+            rec[f"{ex}_inner_s{s}"] = _flat(inner.parameters())
+            rec[f"{ex}_avg_s{s}"] = _flat(p.grad for p in outer.parameters())
+        m.close()
+    np.savez(os.path.join(out, "mirror.npz"), **rec)
+    dist.destroy_process_group()
+
+
+def test_rccl_single_rank_device_mirror_exchanges():
+    out = tempfile.mkdtemp(prefix="dl_rccl_mirror_")
+    mp.spawn(_worker_mirror, args=(_free_port(), out), nprocs=1, join=True)
+    rec = dict(np.load(os.path.join(out, "mirror.npz")))
+    g = load_npz("micro_n1.npz")
+    for ex in ("replicated", "sharded", "a2a"):
+        assert rec[f"{ex}_buckets"][0] > 2, ex
+        for s in (1, 2):
+            assert rec[f"{ex}_inflight_s{s}"][0], ex
+            assert rec[f"{ex}_sharded_s{s}"][0] == (ex != "replicated"), ex
+            for k in ("theta", "buf"):
+                assert rec[f"{ex}_{k}_s{s}"].tobytes() == g[f"{k}_s{s}"].tobytes(), (ex, k, s)
+            assert rec[f"{ex}_inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (ex, s)
+            assert rec[f"{ex}_avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes(), (ex, s)
