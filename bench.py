@@ -155,7 +155,10 @@ def dropin_bpp(ws, exchange, wire="f32"):
     return 12 + 20.0 / ws + 8
 
 
-def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange):
+def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange, placement=None):
+    """The objects src/train.py builds for the outer step (train.py:375-421): an inner model on
+    the GPU, get_outer_model(inner) -- by default the reference's host placement, stepped on an
+    HBM twin (write_back="lazy") -- get_optimizer(outer, nesterov cfg), TrainingComm."""
     from types import SimpleNamespace
 
     from diloco_amd.comm import TrainingComm
@@ -175,7 +178,7 @@ def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange):
     if bucket_elems is not None:
         os.environ[knob] = str(int(bucket_elems))
     try:
-        outer = get_outer_model(inner, "device", fused=True, wire=wire, exchange=exchange)
+        outer = get_outer_model(inner, placement, wire=wire, exchange=exchange)
     finally:
         if bucket_elems is not None:
             if prev is None:
@@ -191,16 +194,18 @@ def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange):
 
 
 def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None,
-               exchange="sharded", cold=False, synced=False):
-    """The outer step through the reference's call surface, src/train.py:263-269, on the fused
-    device outer model: K steps back to back between barrier + synchronize (the four Python
-    calls of step k+1 are issued while step k's kernels run). synced: a device synchronize
-    after every step, as the reference's loop has around its outer step (src/train.py:244),
-    so the calls' host time is exposed. cold (N = 1): then K more steps, each after an
-    Infinity-Cache scrub outside the events."""
+               exchange="sharded", cold=False, synced=False, placement=None):
+    """The outer step through the reference's call surface, src/train.py:263-269, on the outer
+    model get_outer_model returns (placement None: the default, the reference's CPU outer
+    model stepped on its HBM twin; "device": the outer model in HBM): K steps back to back
+    between barrier + synchronize (the four Python calls of step k+1 are issued while step k's
+    kernels run). synced: a device synchronize after every step, as the reference's loop has
+    around its outer step (src/train.py:244), so the calls' host time is exposed. cold (N = 1):
+    then K more steps, each after an Infinity-Cache scrub outside the events."""
     from diloco_amd.utils import compute_pseudo_gradient, sync_inner_model
 
-    inner, outer, opt, comm = _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange)
+    inner, outer, opt, comm = _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange,
+                                              placement)
 
     def one():
         compute_pseudo_gradient(inner, outer)
@@ -223,14 +228,16 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
     dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
     loop_ms = ev[0].elapsed_time(ev[1]) / steps
     P = spec.total()
-    m = outer._diloco_mirror
+    mm = outer._diloco_mirror
+    m = getattr(mm, "dev", mm)  # the lazy host placement steps on its HBM twin
     ex = "replicated" if wire == "bf16" else m.exchange  # the bf16 wire: RCCL's bf16 all_reduce
     bpp = dropin_bpp(ws, ex, wire)
     res = {"tree": spec.name, "params": P, "tensors": len(m.params), "padded": m.tree.total,
            "buckets": m.tree.n_buckets, "ms_per_step": dt * 1e3, "value": 4.0 * P / dt / 1e9,
            "value_aggregate": ws * 4.0 * P / dt / 1e9, "loop_gpu_ms_per_step": round(loop_ms, 5),
            "wire": wire, "exchange": ex if ws > 1 else "none (one peer)",
-           "hbm_bytes_per_param": round(bpp, 3), "synced": synced}
+           "hbm_bytes_per_param": round(bpp, 3), "synced": synced,
+           "placement": ("device" if mm is m else "host (write_back lazy: HBM twin)")}
     if ws == 1:
         # one kernel per step: its average launch duration is the timed loop's GPU span / K
         # (the rocprofv3 average of the same command agrees, profiles/), <= ms_per_step
@@ -253,8 +260,8 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
                                    "outside the events); the four calls' event span"}
     else:
         res["roofline"] = exchange_roofline(m, ws, dev, steps, comm.dp.dp_group(dev))
-    m.close()
-    del outer, opt, inner, m
+    mm.close()
+    del outer, opt, inner, m, mm
     torch.cuda.empty_cache()
     return res
 
@@ -644,13 +651,13 @@ def parity_dropin_exchanges(dev, ws, rank):
         inner, outer, opt, comm = _dropin_objects(spec, dev, rank, "f32", 1 << 20, ex)
         for s in (1, 2):
             if s > 1:
-                synth.inner_tree_device([p.data.view(-1) for p in outer.parameters()], s, rank,
-                                        out=[p.data.view(-1) for p in inner.parameters()])
+                synth.inner_tree_device([p.data.view(-1).to(dev) for p in outer.parameters()], s,
+                                        rank, out=[p.data.view(-1) for p in inner.parameters()])
             compute_pseudo_gradient(inner, outer)
             comm.sync_gradients(outer)
             opt.step()
             sync_inner_model(outer, inner)
-        flat = {k: torch.cat([t.detach().reshape(-1) for t in ts]) for k, ts in (
+        flat = {k: torch.cat([t.detach().reshape(-1).to(dev) for t in ts]) for k, ts in (
             ("theta", list(outer.parameters())), ("grad", [p.grad for p in outer.parameters()]),
             ("mom", [opt.state[p]["momentum_buffer"] for p in outer.parameters()]),
             ("inner", list(inner.parameters())))}
@@ -792,7 +799,7 @@ def dropin_pcie(spec, dev, ws, rank, steps):
     inner = torch.nn.Module()
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
-    outer = get_outer_model(inner, "host", write_back="sync")
+    outer = get_outer_model(inner, "host", write_back="sync")  # host tensors authoritative
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
@@ -1105,6 +1112,7 @@ def assemble_line(meta, head, cpu, legs, parity, exch=None, extra=None):
         "dtype": "f32",
         "data": "synthetic (counter-based GPT-2-shaped tree, SURVEY.md §8d)",
         "config": {"workload": meta["workload"][:300], "tree": head["tree"],
+                   "placement": head.get("placement"),
                    "params": head["params"], "tensors": head["tensors"], "wire": head["wire"],
                    "buckets": head["buckets"], "exchange": head["exchange"],
                    "hbm_bytes_per_param": head["hbm_bytes_per_param"],
@@ -1280,7 +1288,8 @@ def main():
     # the headline: the reference's four calls on the fused device outer model
     head = run_dropin(spec, dev, ws, rank, a.steps, a.warmup, cold=ws == 1 and not a.only_headline)
     workload = (f"DiLoCo outer step, {spec.name} tree per rank, through the reference's calls "
-                "(src/train.py:263-269) on the fused device-resident outer model: "
+                "(src/train.py:263-269) on get_outer_model's default (CPU) outer model, stepped "
+                "on its HBM twin: "
                 + ("per bucket dl_delta_pack -> RCCL reduce_scatter; dl_shard_sgd on this "
                    "rank's 1/n -> RCCL all_gather(theta) -> dl_scatter to inner" if ws > 1 else
                    "one dl_delta_pack_sgd per step (delta + outer.grad + Nesterov SGD + copy "
@@ -1332,6 +1341,8 @@ def main():
                 leg(f"{es.name}_bf16", run_engine, es, dev, ws, rank, ks, 1, torch.bfloat16, cap,
                     False)
                 leg(f"{es.name}_int8", run_q8, es, dev, ws, rank, ks, 1, cap)
+            leg(f"{spec.name}_dropin_device", run_dropin, spec, dev, ws, rank, a.steps,
+                a.warmup, "f32", None, "sharded", False, False, "device")
             leg(f"{spec.name}_dropin_synced", run_dropin, spec, dev, ws, rank, 10, 1, "f32",
                 None, "sharded", False, True)
             leg("dropin_pcie", dropin_pcie, spec, dev, ws, rank, 5)

@@ -55,7 +55,7 @@ def _check_host_params(params: Sequence[torch.Tensor]) -> None:
             raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
 
 
-WRITE_BACKS = ("sync", "deferred")
+WRITE_BACKS = ("lazy", "sync", "deferred")
 OUTER_WIRES = ("f32", "bf16")
 # The DP exchange behind sync_gradients for the device outer model at N > 1:
 #   "sharded"     per bucket RCCL reduce_scatter -> Nesterov SGD on this rank's 1/n of θ and
@@ -106,7 +106,7 @@ def shardable(tree, n: int) -> bool:
 class HostOuterMirror:
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
                  bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, write_back: str = "sync"):
-        if write_back not in WRITE_BACKS:
+        if write_back not in ("sync", "deferred"):
             raise ValueError(f"write_back {write_back!r}: one of {WRITE_BACKS}")
         self.params: List[torch.nn.Parameter] = list(outer_model.parameters())
         if not self.params:
@@ -1135,3 +1135,343 @@ class DeviceOuterMirror:
     def close(self) -> None:
         self._join()
         self.tree.close()
+
+
+# ---- the reference's host placement, kept lazily (write_back="lazy", the default) ----------------
+_NO_TF = torch._C.DisableTorchFunctionSubclass
+
+
+def _to_host_of(args, kwargs) -> None:
+    """Every lazy host object among a torch function's arguments: its arena made current."""
+    seen = set()
+
+    def visit(x):
+        if isinstance(x, (HostParameter, HostTensor)):
+            d = x.__dict__
+            r = d.get("_dl_mirror")
+            m = r() if r is not None else None
+            key = (id(m), d.get("_dl_arena"))
+            if m is not None and key not in seen:
+                seen.add(key)
+                m.to_host(d["_dl_arena"])
+        elif isinstance(x, (list, tuple)):
+            for y in x:
+                visit(y)
+
+    visit(args)
+    if kwargs:
+        visit(tuple(kwargs.values()))
+
+
+class HostTensor(torch.Tensor):
+    """`.grad` or `outer_optimizer.state[p]["momentum_buffer"]` of the host-placed outer model
+    under write_back="lazy": a CPU tensor (a view of a pinned host arena) whose values are
+    copied from HBM the first time anything reads them after the device changed them -- any
+    torch function other than a metadata query, pickling, deep copy. Results of operations are
+    plain tensors."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        if func not in _META:
+            _to_host_of(args, kwargs)
+        with _NO_TF():
+            return func(*args, **(kwargs or {}))
+
+    def _plain(self) -> torch.Tensor:
+        _to_host_of((self,), None)
+        with _NO_TF():
+            return self.detach().clone()
+
+    def __deepcopy__(self, memo):
+        if id(self) in memo:
+            return memo[id(self)]
+        out = self._plain()
+        memo[id(self)] = out
+        return out
+
+    def __reduce_ex__(self, proto):
+        return self._plain().__reduce_ex__(proto)
+
+
+class HostParameter(torch.nn.Parameter):
+    """A parameter of the host-placed outer model (src/utils.py:216: a CPU tensor) under
+    write_back="lazy". The outer step runs on its HBM twin (mirror.LazyHostOuterMirror); this
+    object -- the same Parameter object get_outer_model returned, its class switched in place,
+    so the optimizer's references stay valid -- holds a view of a pinned host arena that is
+    brought up to date from HBM when it is read: any torch function on it other than a metadata
+    query, `.data`, `.grad`, pickling, deep copy. Writes (in place, through `.data`, assigning
+    `.data` or `.grad`) are uploaded before the next outer-step call."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        if func not in _META:
+            _to_host_of(args, kwargs)
+        with _NO_TF():
+            return func(*args, **(kwargs or {}))
+
+    def _m(self):
+        r = self.__dict__.get("_dl_mirror")
+        return r() if r is not None else None
+
+    @property
+    def data(self):
+        m = self._m()
+        if m is not None:
+            m.to_host("theta")
+        with _NO_TF():
+            return _DATA.__get__(self)
+
+    @data.setter
+    def data(self, value):
+        m = self._m()
+        if m is not None:
+            m.to_host("theta")
+            m.theta_touched = True
+        with _NO_TF():
+            _DATA.__set__(self, value)
+
+    @property
+    def grad(self):
+        m = self._m()
+        if m is not None:
+            m.to_host("grad")
+        with _NO_TF():
+            return _GRAD.__get__(self)
+
+    @grad.setter
+    def grad(self, value):
+        m = self._m()
+        if m is not None:
+            m.to_host("grad")
+            m.grads_touched = True
+        with _NO_TF():
+            _GRAD.__set__(self, value)
+
+    @grad.deleter
+    def grad(self):
+        m = self._m()
+        if m is not None:
+            m.to_host("grad")
+            m.grads_touched = True
+        with _NO_TF():
+            _GRAD.__delete__(self)
+
+    def __reduce_ex__(self, proto):  # pickles as a plain Parameter of the current values
+        return (torch._utils._rebuild_parameter, (self.data, self.requires_grad, OrderedDict()))
+
+    def __deepcopy__(self, memo):
+        if id(self) in memo:
+            return memo[id(self)]
+        out = torch.nn.Parameter(self.data.clone(), self.requires_grad)
+        memo[id(self)] = out
+        return out
+
+
+_ARENAS = ("grad", "theta", "mom")
+
+
+class LazyHostOuterMirror:
+    """The reference's host-resident outer model (get_outer_model -> deepcopy(inner).to("cpu"),
+    src/utils.py:213-216) stepped at device speed: write_back="lazy", the default placement.
+
+    The outer model's parameters stay the CPU Parameters the reference returns, their .grad
+    and the optimizer's momentum buffers CPU tensors -- views of three pinned host arenas
+    (θ, grad, momentum) laid out like the device's. The outer step itself runs on an HBM twin
+    of the outer model (a DeviceOuterMirror: the fused one-pass kernel at one peer, the sharded
+    RCCL exchange at N > 1, no PCIe traffic per step). A host arena is copied from HBM (one
+    DMA) only when something reads one of its tensors after the device changed it
+    (HostParameter / HostTensor intercept every read), and host-side writes are uploaded before
+    the next outer-step call (detected by the arenas' version counters and by assignments of
+    `.data` / `.grad`). So every value a caller observes is the reference's, on the CPU,
+    while an outer step that nobody observes costs what the device placement costs. Reading
+    `.grad` or the momentum under the sharded exchange at N > 1 is a collective over the DP
+    group, as for the device placement."""
+
+    def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
+                 bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = True,
+                 wire: str = "f32", exchange: str = "sharded"):
+        self.device = torch.device(device)
+        params = module_params(outer_model)
+        if not params:
+            raise ValueError("outer model has no parameters")
+        _check_host_params(params)
+        with _NO_TF():
+            twin = torch.nn.Module()
+            twin.ps = torch.nn.ParameterList([
+                torch.nn.Parameter(_DATA.__get__(p).to(self.device), p.requires_grad)
+                for p in params])
+        self.dev = DeviceOuterMirror(twin, self.device, kernels, bucket_cap_elems, fused, wire,
+                                     exchange)
+        self._twin = twin
+        self.fused, self.wire, self.exchange = fused, wire, exchange
+        self.tree, self.offs, self.numels = self.dev.tree, self.dev.offs, self.dev.numels
+        pin = self.device.type == "cuda"
+        z = dict(dtype=torch.float32, pin_memory=pin)
+        self.h = {"theta": torch.zeros(self.tree.total, **z),
+                  "grad": torch.zeros(self.tree.total, **z), "mom": None}
+        self._pin = pin
+        ref = weakref.ref(self)
+        with _NO_TF(), torch.no_grad():
+            self._theta_views = self._views(self.h["theta"])
+            for p, v in zip(params, self._theta_views):
+                v.copy_(_DATA.__get__(p))
+                _DATA.__set__(p, v)
+                p.__class__ = HostParameter  # same object: the optimizer's references stay
+                p.__dict__["_dl_mirror"] = ref
+                p.__dict__["_dl_arena"] = "theta"
+            self._grad_views = [self._host_tensor(v, "grad") for v in self._views(self.h["grad"])]
+        self.params = params
+        self._mom_views: Optional[List[torch.Tensor]] = None
+        self._ver = {"theta": self.h["theta"]._version, "grad": self.h["grad"]._version,
+                     "mom": None}
+        self._dirty: set = set()
+        self._grads_set = False  # the API .grads are the grad arena's views
+        self.theta_touched = self.grads_touched = False
+
+    def _views(self, arena: torch.Tensor) -> List[torch.Tensor]:
+        return [arena[o:o + n].view(p.shape)
+                for o, n, p in zip(self.offs, self.numels, self.dev.params)]
+
+    def _host_tensor(self, view: torch.Tensor, arena: str) -> "HostTensor":
+        t = view.as_subclass(HostTensor)
+        t.__dict__["_dl_mirror"] = weakref.ref(self)
+        t.__dict__["_dl_arena"] = arena
+        return t
+
+    @property
+    def pending(self) -> bool:
+        return bool(self._dirty)
+
+    # ---- coherence ------------------------------------------------------------------------
+    def _sync_stream(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def to_host(self, arena: str) -> None:
+        """The host arena equals the device state (one DMA if the device changed it)."""
+        if arena not in self._dirty:
+            return
+        with _NO_TF():
+            if arena == "grad":
+                self.dev.settle_grads()  # the pending delta / Σ / sharded gathers, then /n
+            elif arena == "mom":
+                self.dev.gather_momentum()
+            src = {"theta": self.dev.d_theta, "grad": self.dev.d_wire, "mom": self.dev.d_mom}[arena]
+            h = self.h[arena]
+            h.copy_(src, non_blocking=self._pin)
+            self._sync_stream()
+            self._dirty.discard(arena)
+            self._ver[arena] = h._version
+
+    def flush(self) -> None:
+        for a in _ARENAS:
+            self.to_host(a)
+
+    def invalidate(self) -> None:
+        self.dev.invalidate()
+        self.theta_touched = self.grads_touched = True
+
+    def _changed(self, arena: str, what: str) -> bool:
+        h = self.h[arena]
+        if h is None or h._version == self._ver[arena]:
+            return False
+        if arena in self._dirty:
+            raise RuntimeError(
+                f"the host {what} were written while their device copy was newer (a write that "
+                "bypassed the outer model's tensors); call flush_outer_model() first")
+        return True
+
+    def _push(self) -> None:
+        """Host writes since the last call -> HBM (before any outer-step work)."""
+        dev = self.dev
+        with _NO_TF(), torch.no_grad():
+            if self.theta_touched:  # a parameter's .data was assigned: back into the arena
+                self.theta_touched = False
+                for p, v in zip(self.params, self._theta_views):
+                    cur = _DATA.__get__(p)
+                    if cur.data_ptr() != v.data_ptr():
+                        v.copy_(cur)
+                        _DATA.__set__(p, v)
+            if self._changed("theta", "outer parameters"):
+                dev.d_theta.copy_(self.h["theta"], non_blocking=self._pin)
+                self._ver["theta"] = self.h["theta"]._version
+            if self.grads_touched:  # a .grad was assigned: values into the arena, or None
+                self.grads_touched = False
+                self._grads_set = False
+                for i, (p, tp) in enumerate(zip(self.params, dev.params)):
+                    g, v = _GRAD.__get__(p), self._grad_views[i]
+                    if g is None:
+                        _GRAD.__set__(tp, None)
+                        dev.grads_touched = True
+                        continue
+                    if g is not v:
+                        if g.data_ptr() != v.data_ptr():
+                            v.copy_(g)
+                        _GRAD.__set__(p, v)
+                    if _GRAD.__get__(tp) is None:
+                        _GRAD.__set__(tp, dev._views["wire"][i])
+                        dev.grads_touched = True
+            if self._changed("grad", "outer gradients"):
+                dev.d_wire.copy_(self.h["grad"], non_blocking=self._pin)
+                self._ver["grad"] = self.h["grad"]._version
+                dev.grads_touched = True
+
+    def _set_api_grads(self) -> None:
+        if self._grads_set:
+            return
+        with _NO_TF():
+            for p, v in zip(self.params, self._grad_views):
+                if _GRAD.__get__(p) is not v:
+                    _GRAD.__set__(p, v)
+        self._grads_set = True
+
+    # ---- the four reference operations --------------------------------------------------
+    def pseudo_gradient(self, inner_params: Sequence[torch.Tensor]) -> None:
+        self._push()
+        self.dev.pseudo_gradient(inner_params)
+        self._set_api_grads()
+        self._dirty.add("grad")
+
+    def all_reduce(self, group, num_peers: int, ordered: bool = False) -> None:
+        self._push()
+        self.dev.all_reduce(group, num_peers, ordered)
+        self._set_api_grads()
+        self._dirty.add("grad")
+
+    def sgd_step(self, lr: float, momentum: float, nesterov: bool, host_bufs):
+        self._push()
+        dev = self.dev
+        dev_bufs = host_bufs
+        if momentum != 0 and self._mom_views is not None and len(host_bufs) == len(
+                self._mom_views) and all(map(is_, host_bufs, self._mom_views)):
+            if self._changed("mom", "momentum buffers"):  # written on the host: upload
+                with _NO_TF():
+                    dev.d_mom.copy_(self.h["mom"], non_blocking=self._pin)
+                self._ver["mom"] = self.h["mom"]._version
+                dev._mom_stale = False
+            dev_bufs = dev._views["mom"]  # the device's own buffers: not the first step
+        dev.sgd_step(lr, momentum, nesterov, dev_bufs)
+        self._dirty.add("theta")
+        if momentum == 0:
+            return [None] * len(self.params)
+        if self._mom_views is None:
+            self.h["mom"] = torch.zeros(self.tree.total, dtype=torch.float32,
+                                        pin_memory=self._pin)
+            self._mom_views = [self._host_tensor(v, "mom") for v in self._views(self.h["mom"])]
+            self._ver["mom"] = self.h["mom"]._version
+        self._dirty.add("mom")
+        return self._mom_views
+
+    def copy_to_inner(self, inner_params: Sequence[torch.Tensor]) -> None:
+        self._push()
+        self.dev.copy_to_inner(inner_params)
+
+    def close(self) -> None:
+        self.flush()
+        self.dev.close()
+
+    def __deepcopy__(self, memo):  # a copied outer model starts without a mirror
+        return None
+
+    def __reduce_ex__(self, proto):
+        return (_none, ())

@@ -16,30 +16,33 @@ Placement of the outer model (`get_outer_model(..., placement=)`, default from t
 DILOCO_OUTER_PLACEMENT environment variable, "host" if unset):
 
   "host"    the reference's placement: a CPU module whose parameters, gradients and momentum
-            buffers hold exactly the reference's values; a device mirror
-            (mirror.HostOuterMirror) keeps packed copies in HBM coherent with them (one
-            pinned DMA per arena per step).
+            buffers hold exactly the reference's values whenever they are read. Write-back
+            (`get_outer_model(..., write_back=)`, default from DILOCO_HOST_WRITEBACK):
+              "lazy" (default)  the outer step runs on an HBM twin of the outer model
+                        (mirror.LazyHostOuterMirror around a DeviceOuterMirror: the same
+                        kernels and exchange as "device" below, no PCIe traffic per step);
+                        the CPU tensors are views of pinned arenas refreshed from HBM when
+                        something reads them (mirror.HostParameter / HostTensor), and host
+                        writes are uploaded before the next call;
+              "sync"    the host tensors are authoritative: every call ends with them
+                        updated, one pinned DMA per arena (mirror.HostOuterMirror);
+              "deferred"  as "sync", the step's write-back issued by sync_inner_model in one
+                        batch of DMAs and not waited for (flush_outer_model / state_dict()
+                        wait for it).
   "device"  SURVEY §8f row 2: the outer module lives on the inner model's GPU, its parameters,
             .grad and momentum buffers are views of packed HBM arenas
-            (mirror.DeviceOuterMirror); no PCIe traffic and no host synchronisation per outer
-            step. Host copies are made lazily by torch (`.cpu()`, `state_dict()`).
-            fused (`get_outer_model(..., fused=)`, default from DILOCO_OUTER_FUSED, on if
-            unset): the four calls run as one HBM pass at one peer (dl_delta_pack_sgd, the
-            engine's kernel) and pack -> RCCL -> one SGD pass at N > 1; the parameters are
-            mirror.OuterParameter, whose .grad completes the deferred work when read, and
-            sync_inner_model is a verified no-op after the step (see DeviceOuterMirror).
-            wire (`get_outer_model(..., wire=)`, default from DILOCO_OUTER_WIRE, "f32"):
-            "bf16" sends the deltas over the DP exchange in bf16 (BASELINE config #5: the cast
-            in the pack kernel, the SGD fused into the unpack); .grad then shows the codec's
-            decoded average.
+            (mirror.DeviceOuterMirror); host copies are made by torch on demand (`.cpu()`).
 
-Write-back of the host placement (`get_outer_model(..., write_back=)`, default from
-DILOCO_HOST_WRITEBACK, "sync" if unset): "sync" -- every call returns with the host tensors
-updated, as the reference's do; "deferred" -- the device copy stays authoritative through the
-outer step and the step's results reach the host tensors in one batch of DMAs issued by
-sync_inner_model and not waited for, so the PCIe transfer overlaps the next inner steps
-(mirror.HostOuterMirror; `flush_outer_model`, the outer model's `state_dict()` and
-`OuterSGD.state_dict()` wait for it).
+For "device" and "host"/"lazy": fused (`get_outer_model(..., fused=)`, DILOCO_OUTER_FUSED, on
+if unset) runs the four calls as one HBM pass at one peer (dl_delta_pack_sgd) and as
+pack -> exchange -> one SGD pass at N > 1, with .grad completing the deferred work when read
+and sync_inner_model a verified no-op after the step; wire (DILOCO_OUTER_WIRE, "f32";
+"bf16": BASELINE config #5's codec on the DP exchange); exchange (DILOCO_OUTER_EXCHANGE,
+"sharded": reduce_scatter -> SGD on this rank's 1/n -> all_gather of θ, SURVEY §8e;
+"replicated": all_reduce -> the SGD pass on every rank; "a2a": the sharded form with a
+rank-order sum, bit-exact at every n; DILOCO_DP_EXCHANGE=a2a selects it too). Under the
+sharded forms a read of .grad or of the momentum buffers at N > 1 gathers them from the peers:
+a collective over the DP group, made by every rank.
 """
 from __future__ import annotations
 
@@ -52,7 +55,7 @@ from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
 from .mirror import (OUTER_EXCHANGES, OUTER_WIRES, WRITE_BACKS, DeviceOuterMirror,
-                     HostOuterMirror, module_params)
+                     HostOuterMirror, LazyHostOuterMirror, module_params)
 from .optim import OuterSGD
 from .plan import DEFAULT_BUCKET_CAP_ELEMS
 
@@ -116,8 +119,16 @@ def outer_mirror(outer_model: nn.Module, device=None):
                 if not torch.cuda.is_available():
                     raise RuntimeError("the DiLoCo outer step runs on the GPU; no HIP device")
                 device = torch.device("cuda", torch.cuda.current_device())
-        m = HostOuterMirror(outer_model, torch.device(device), kernels=k,
-                            write_back=getattr(outer_model, _WRITE_BACK, "sync"))
+        wb = getattr(outer_model, _WRITE_BACK, "lazy")
+        if wb == "lazy":
+            cap = int(os.environ.get("DILOCO_OUTER_BUCKET_ELEMS", DEFAULT_BUCKET_CAP_ELEMS))
+            m = LazyHostOuterMirror(outer_model, torch.device(device), kernels=k,
+                                    bucket_cap_elems=cap,
+                                    fused=getattr(outer_model, _FUSED, True),
+                                    wire=getattr(outer_model, _WIRE, "f32"),
+                                    exchange=getattr(outer_model, _EXCHANGE, "sharded"))
+        else:
+            m = HostOuterMirror(outer_model, torch.device(device), kernels=k, write_back=wb)
         object.__setattr__(outer_model, _ATTR, m)  # not a submodule / not in state_dict
     return m
 
@@ -143,7 +154,7 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     if placement not in PLACEMENTS:
         raise ValueError(f"placement {placement!r}: one of {PLACEMENTS}")
     if write_back is None:
-        write_back = os.environ.get("DILOCO_HOST_WRITEBACK", "sync")
+        write_back = os.environ.get("DILOCO_HOST_WRITEBACK", "lazy")
     if write_back not in WRITE_BACKS:
         raise ValueError(f"write_back {write_back!r}: one of {WRITE_BACKS}")
     if fused is None:
@@ -156,9 +167,10 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
         exchange = os.environ.get("DILOCO_OUTER_EXCHANGE", "sharded")
     if exchange not in OUTER_EXCHANGES:
         raise ValueError(f"exchange {exchange!r}: one of {OUTER_EXCHANGES}")
-    if wire != "f32" and placement != "device":
-        raise ValueError("the bf16 outer wire needs placement='device' (the host placement "
-                         "keeps the reference's fp32 host tensors end to end)")
+    lazy = placement == "device" or write_back == "lazy"  # the outer step runs on an HBM copy
+    if wire != "f32" and not lazy:
+        raise ValueError("the bf16 outer wire needs placement='device' or write_back='lazy' "
+                         "(write_back 'sync' / 'deferred' keep the host tensors authoritative)")
     outer_model = copy.deepcopy(inner_model)
     has_params = next(inner_model.parameters(), None) is not None
     if placement == "host":
@@ -176,13 +188,18 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     object.__setattr__(outer_model, _OUTER, True)  # get_optimizer: SGD here is the outer SGD
     object.__setattr__(outer_model, _PLACEMENT, placement)
     object.__setattr__(outer_model, _WRITE_BACK, write_back)
-    object.__setattr__(outer_model, _FUSED, bool(fused) and placement == "device")
+    object.__setattr__(outer_model, _FUSED, bool(fused) and lazy)
     object.__setattr__(outer_model, _WIRE, wire)
     object.__setattr__(outer_model, _EXCHANGE, exchange)
     if placement == "device" and has_params:
         # lay the parameters out in the packed HBM arena now (fused: as OuterParameters);
         # a model without parameters keeps none: the four calls are the reference's empty loops
         outer_mirror(outer_model)
+    elif write_back == "lazy" and has_params and device_path(next(inner_model.parameters())):
+        # the inner model is on its GPU already: the HBM twin now (the reference builds the
+        # outer model before moving the inner one, src/train.py:382; then the first
+        # compute_pseudo_gradient creates it)
+        outer_mirror(outer_model, _inner_device(inner_model))
     elif write_back == "deferred":
         # a checkpoint of the outer model waits for the write-back in flight
         outer_model.register_state_dict_pre_hook(lambda mod, prefix, keep_vars:

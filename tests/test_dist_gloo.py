@@ -76,7 +76,8 @@ def _worker(rank, world, port, mode, num_stages, out):
                 "dropin_device_bf16_eager", "dropin_device_quiet_buckets",
                 "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
                 "dropin_device_a2a_dp", "dropin_a2a_dp", "dropin_device_momentum_first",
-                "dropin_device_eager_a2a_dp"):
+                "dropin_device_eager_a2a_dp", "dropin_sync", "dropin_sync_a2a_dp",
+                "dropin_quiet"):
         if mode in ("dropin_device_quiet_buckets", "dropin_device_quiet_a2a",
                     "dropin_device_momentum_first"):  # the exchange in several buckets: the
             os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # SGD waits bucket by bucket
@@ -89,15 +90,18 @@ def _worker(rank, world, port, mode, num_stages, out):
         from diloco_amd.utils import flush_outer_model, has_mirror
 
         deferred = mode == "dropin_deferred"
+        # dropin / dropin_quiet / dropin_a2a_dp: the default host placement (write_back "lazy",
+        # the outer step on an HBM twin); dropin_sync*: the host tensors authoritative
+        sync = mode.startswith("dropin_sync")
         # quiet: nothing reads the outer model between the four calls (src/train.py:261-269),
         # so the fused device model defers the delta and the /n into its one SGD pass
         quiet = mode in ("dropin_device_quiet", "dropin_device_bf16", "dropin_device_quiet_buckets",
                          "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
-                         "dropin_device_a2a_dp", "dropin_device_momentum_first")
+                         "dropin_device_a2a_dp", "dropin_device_momentum_first", "dropin_quiet")
         device = mode.startswith("dropin_device")
         inner = _micro_module(theta0, shapes)
         outer = get_outer_model(inner, placement="device" if device else None,
-                                write_back="deferred" if deferred else None,
+                                write_back="deferred" if deferred else "sync" if sync else None,
                                 fused="_eager" not in mode,
                                 wire="bf16" if "bf16" in mode else None, exchange=exchange)
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
@@ -107,7 +111,8 @@ def _worker(rank, world, port, mode, num_stages, out):
             assert not has_mirror(outer)
         else:
             assert type(outer_mirror(outer)).__name__ == (
-                "DeviceOuterMirror" if device else "HostOuterMirror")
+                "DeviceOuterMirror" if device else
+                "HostOuterMirror" if (sync or deferred) else "LazyHostOuterMirror")
             if device:
                 assert outer_mirror(outer).fused == ("_eager" not in mode)
                 if "DILOCO_OUTER_BUCKET_ELEMS" in os.environ:
@@ -138,8 +143,9 @@ def _worker(rank, world, port, mode, num_stages, out):
             elif deferred and len(world_.dp_ranks) > 1:  # the host still has step 1's averages
                 assert host(p.grad for p in outer.parameters()).tobytes() == rec["avg_s1"].tobytes()
             opt.step()
-            if device and quiet and len(world_.dp_ranks) > 1:  # which exchange the step ran
+            if quiet and len(world_.dp_ranks) > 1:  # which exchange the step ran
                 m = outer_mirror(outer)
+                m = getattr(m, "dev", m)  # the lazy host placement's HBM twin
                 rec["sharded_step"] = np.array([m._mom_stale, m._xmode is not None])
             if deferred and s == 1:
                 flush_outer_model(outer)
@@ -325,7 +331,8 @@ def _run(mode, world, num_stages=1):
                                   "dropin_device_quiet_buckets", "dropin_device_quiet_replicated",
                                   "dropin_device_quiet_a2a", "dropin_device_a2a_dp",
                                   "dropin_a2a_dp", "dropin_device_momentum_first",
-                                  "dropin_device_eager_a2a_dp",
+                                  "dropin_device_eager_a2a_dp", "dropin_sync", "dropin_quiet",
+                                  "dropin_sync_a2a_dp",
                                   "dropin_device_eager", "dropin_deferred", "engine",
                                   "engine_ar", "engine_a2a", "dropin_host"])
 def test_two_peers_match_reference_bit_exact(mode):
@@ -347,7 +354,8 @@ def test_two_peers_match_reference_bit_exact(mode):
 
 
 @pytest.mark.parametrize("mode", ["dropin_device_quiet_a2a", "dropin_device_a2a_dp",
-                                  "dropin_a2a_dp", "dropin_device_eager_a2a_dp"])
+                                  "dropin_a2a_dp", "dropin_device_eager_a2a_dp",
+                                  "dropin_sync_a2a_dp"])
 @pytest.mark.parametrize("world", [4, 8])
 def test_dropin_ordered_exchange_is_bit_exact_at_any_n(mode, world):
     """The outer model's ordered exchange (get_outer_model(..., exchange="a2a"), or
@@ -369,6 +377,7 @@ def test_dropin_ordered_exchange_is_bit_exact_at_any_n(mode, world):
                                         ("dropin_device_quiet_buckets", 4),
                                         ("dropin_device_quiet_buckets", 8),
                                         ("dropin_device_momentum_first", 8),
+                                        ("dropin_quiet", 8), ("dropin_sync", 4),
                                         ("dropin_device_quiet_replicated", 4)])
 def test_four_and_eight_peers_match_reference_normwise(mode, world):
     """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""

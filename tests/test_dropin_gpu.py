@@ -130,12 +130,15 @@ def _init_single():
     (False, "host", "sync", False, None), (True, "host", "sync", False, None),
     (False, "device", "sync", False, True), (False, "device", "sync", True, True),
     (False, "device", "sync", False, False), (True, "device", "sync", True, True),
-    (False, "host", "deferred", False, None)])
+    (False, "host", "deferred", False, None), (False, "host", "lazy", False, None),
+    (False, "host", "lazy", True, None), (True, "host", "lazy", True, None),
+    (False, "host", "lazy", True, False)])
 def test_dropin_single_peer_matches_reference(stock_sgd, placement, write_back, quiet, fused):
     """The reference's call sequence, outer model on the host (its placement) or in HBM
     (placement="device"); torch's own CPU SGD on the host outer model as
     well (the mirror must see its in-place updates); the host placement with the deferred
-    write-back (side-stream DMAs issued by sync_inner_model)."""
+    write-back (side-stream DMAs issued by sync_inner_model) and with the lazy one (the
+    default: the step on the HBM twin, host tensors refreshed when read)."""
     _init_single()
     g = load_npz("micro_n1.npz")
     rec = _outer_steps(0, 1, stock_sgd=stock_sgd, placement=placement, write_back=write_back,

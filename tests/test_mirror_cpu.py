@@ -127,12 +127,112 @@ def test_host_write_while_device_is_newer_is_an_error(what):
     opt2.step()
 
 
-def test_sync_write_back_is_the_default_and_argument_errors():
+def test_lazy_write_back_is_the_default_and_argument_errors():
+    from diloco_amd.mirror import HostParameter, LazyHostOuterMirror
+
     inner, outer = _models(None)
+    before = list(outer.parameters())
+    compute_pseudo_gradient(inner, outer)
+    assert isinstance(outer._diloco_mirror, LazyHostOuterMirror)
+    # the same Parameter objects, on the CPU, their class switched in place
+    assert all(a is b for a, b in zip(before, outer.parameters()))
+    assert all(type(p) is HostParameter and p.device.type == "cpu" for p in before)
+    with pytest.raises(ValueError, match="write_back"):
+        get_outer_model(inner, write_back="bogus")
+    inner, outer = _models("sync")
     compute_pseudo_gradient(inner, outer)
     assert not outer._diloco_mirror.deferred
-    with pytest.raises(ValueError, match="write_back"):
-        get_outer_model(inner, write_back="lazy")
+
+
+# ---- the lazy host placement (mirror.LazyHostOuterMirror, write_back="lazy", the default) ----
+@pytest.mark.parametrize("quiet", [True, False])
+def test_lazy_host_model_matches_reference_one_peer(quiet):
+    """src/train.py:263-269 at one peer with the reference's host placement: quiet (nothing
+    read between the calls) runs ONE dl_delta_pack_sgd per outer step on the device twin and no
+    host copy at all; every host tensor read afterwards (params, .grad, momentum) equals the
+    reference's fixture, and reading mid-sequence computes the delta first."""
+    k = _Counting()
+    kernels.set_default_kernels(k)
+    g = load_npz("micro_n1.npz")
+    inner, outer = _models(None)
+    m = outer._diloco_mirror
+    opt = get_optimizer(outer, SGD_CFG)
+    for s in (1, 2):
+        _set_inner(inner, outer, s)
+        k.calls.clear()
+        compute_pseudo_gradient(inner, outer)
+        if not quiet:
+            assert _host(p.grad for p in outer.parameters()).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        opt.step()
+        sync_inner_model(outer, inner)
+        if quiet:
+            assert k.calls == {"delta_pack_sgd": 1}, k.calls
+            assert m._dirty == {"grad", "theta", "mom"}  # nothing copied to the host yet
+        else:
+            assert k.calls == {"delta_pack": 1, "unpack_sgd": 1}, k.calls
+        assert _host(outer.parameters()).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert _host(p.grad for p in outer.parameters()).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+        assert _host(opt.state[p]["momentum_buffer"]
+                     for p in outer.parameters()).tobytes() == g[f"buf_s{s}"].tobytes()
+        assert _host(inner.parameters()).tobytes() == g[f"theta_s{s}"].tobytes()
+        assert not m._dirty
+
+
+def test_lazy_host_writes_reach_the_device_before_the_next_call():
+    """Host-side writes between outer steps -- in place on a parameter, through `.data`,
+    assigning `.data`, in place on a momentum buffer -- are read back from the host arenas
+    before the next call, so the next step is the reference's step of the modified state."""
+    from oracle import oracle
+
+    inner, outer = _models(None)
+    opt = get_optimizer(outer, SGD_CFG)
+    ps = list(outer.parameters())
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    opt.step()
+    sync_inner_model(outer, inner)
+    with torch.no_grad():
+        ps[0].add_(0.25)                       # in place (hooked: flushed first)
+        ps[1].data.mul_(2.0)                   # through .data (version counter)
+        ps[2].data = torch.full_like(ps[2], 0.5)  # .data assigned
+        opt.state[ps[3]]["momentum_buffer"].add_(1.0)
+    theta = [p.detach().numpy().reshape(-1).copy() for p in ps]
+    buf = [opt.state[p]["momentum_buffer"].detach().numpy().reshape(-1).copy() for p in ps]
+    _set_inner(inner, outer, 2)
+    inners = [p.detach().numpy().reshape(-1).copy() for p in inner.parameters()]
+    compute_pseudo_gradient(inner, outer)
+    opt.step()
+    sync_inner_model(outer, inner)
+    for t in range(len(theta)):
+        oracle.sgd(theta[t], buf[t], oracle.delta(theta[t], inners[t]), 0.7, 0.9, True, False)
+    assert _host(outer.parameters()).tobytes() == np.concatenate(theta).tobytes()
+    assert _host(opt.state[p]["momentum_buffer"] for p in ps).tobytes() == np.concatenate(buf).tobytes()
+    assert _host(inner.parameters()).tobytes() == np.concatenate(theta).tobytes()
+
+
+def test_lazy_host_model_checkpoints_and_copies_as_plain_tensors():
+    import copy
+    import io
+
+    g = load_npz("micro_n1.npz")
+    inner, outer = _models(None)
+    opt = get_optimizer(outer, SGD_CFG)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    opt.step()
+    sync_inner_model(outer, inner)
+    c = copy.deepcopy(outer)  # the mirror stays behind; plain Parameters of the values
+    assert all(type(p) is torch.nn.Parameter for p in c.parameters())
+    assert _host(c.parameters()).tobytes() == g["theta_s1"].tobytes()
+    bio = io.BytesIO()
+    torch.save({"model": outer.state_dict(), "opt": opt.state_dict()}, bio)
+    bio.seek(0)
+    sd = torch.load(bio, weights_only=True)
+    assert _host(sd["model"].values()).tobytes() == g["theta_s1"].tobytes()
+    assert _host(sd["opt"]["state"][i]["momentum_buffer"]
+                 for i in range(len(sd["opt"]["state"]))).tobytes() == g["buf_s1"].tobytes()
+    st = copy.deepcopy(dict(opt.state))
+    assert all(type(v["momentum_buffer"]) is torch.Tensor for v in st.values())
 
 
 # ---- the fused device outer model (mirror.DeviceOuterMirror, fused=True) ---------------------
