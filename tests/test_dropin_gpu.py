@@ -831,3 +831,48 @@ def test_t13b_fused_device_dropin_vs_oracle_on_sampled_tensors():
     del outer, inner, opt, ps, qs
     gc.collect()
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("placement", ["device", None])
+def test_outer_model_deepcopies_and_pickles_with_the_hip_library(placement):
+    """an outer model whose mirror holds the HIP library's tree handle (a ctypes
+    pointer) deep-copies and pickles: the mirror stays behind, the copy's parameters are plain
+    Parameters holding the current values (the device placement and the default lazy host
+    placement, after a fused outer step)."""
+    import copy
+    import io
+
+    from diloco_amd import synth
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+
+    g = load_npz("micro_n1.npz")
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cuda:0")
+    outer = get_outer_model(inner, placement)
+    opt = get_optimizer(outer, SGD_CFG)
+    vals = synth.inner_tree([p.detach().cpu().numpy().reshape(-1) for p in outer.parameters()],
+                            1, 0)
+    with torch.no_grad():
+        for p, v in zip(inner.parameters(), vals):
+            p.copy_(torch.from_numpy(v).view(p.shape))
+    compute_pseudo_gradient(inner, outer)
+    opt.step()
+    sync_inner_model(outer, inner)
+    c = copy.deepcopy(outer)
+    assert getattr(c, "_diloco_mirror", None) is None
+    assert all(type(p) is torch.nn.Parameter for p in c.parameters())
+    assert _flat(c.parameters()).tobytes() == g["theta_s1"].tobytes()
+    bio = io.BytesIO()
+    torch.save(outer, bio)  # the whole module object, mirror attribute included
+    bio.seek(0)
+    d = torch.load(bio, weights_only=False)  # our own file, written just above
+    assert getattr(d, "_diloco_mirror", None) is None
+    assert _flat(d.parameters()).tobytes() == g["theta_s1"].tobytes()
+    bio = io.BytesIO()
+    torch.save(opt.state_dict(), bio)
+    bio.seek(0)
+    st = torch.load(bio, weights_only=True)["state"]
+    assert _flat(st[i]["momentum_buffer"] for i in range(len(st))).tobytes() == g["buf_s1"].tobytes()

@@ -465,3 +465,21 @@ def test_module_params_is_parameters_order_by_identity():
     got, exp = module_params(m), list(m.parameters())
     assert len(got) == len(exp)
     assert all(a is b for a, b in zip(got, exp))
+
+
+def test_boolean_knobs_parse_strictly(monkeypatch):
+    """DILOCO_OUTER_FUSED takes 1/0/true/false/on/off/yes/no in any case and
+    raises on anything else (it used to read every value but '0' and '' as on)."""
+    from diloco_amd.utils import env_flag
+
+    for v, want in (("1", True), ("TRUE", True), ("on", True), ("Yes", True), ("0", False),
+                    ("false", False), ("OFF", False), ("no", False), ("", True)):
+        monkeypatch.setenv("DILOCO_OUTER_FUSED", v)
+        assert env_flag("DILOCO_OUTER_FUSED", True) is want, v
+    monkeypatch.setenv("DILOCO_OUTER_FUSED", "nope")
+    with pytest.raises(ValueError, match="DILOCO_OUTER_FUSED"):
+        env_flag("DILOCO_OUTER_FUSED", True)
+    inner, _ = _device_models(True)
+    monkeypatch.setenv("DILOCO_OUTER_FUSED", "off")
+    outer = get_outer_model(inner, placement="device")
+    assert not outer._diloco_mirror.fused
