@@ -1141,19 +1141,22 @@ class DeviceOuterMirror:
 _NO_TF = torch._C.DisableTorchFunctionSubclass
 
 
-def _to_host_of(args, kwargs) -> None:
-    """Every lazy host object among a torch function's arguments: its arena made current."""
-    seen = set()
+def _host_args(args, kwargs) -> list:
+    """The lazy host objects among a torch function's arguments, as (tensor, mirror, arena),
+    each arena made current first."""
+    found, seen = [], set()
 
     def visit(x):
         if isinstance(x, (HostParameter, HostTensor)):
             d = x.__dict__
             r = d.get("_dl_mirror")
             m = r() if r is not None else None
-            key = (id(m), d.get("_dl_arena"))
-            if m is not None and key not in seen:
-                seen.add(key)
-                m.to_host(d["_dl_arena"])
+            if m is not None:
+                arena = d["_dl_arena"]
+                found.append((x, m, arena))
+                if (id(m), arena) not in seen:
+                    seen.add((id(m), arena))
+                    m.to_host(arena)
         elif isinstance(x, (list, tuple)):
             for y in x:
                 visit(y)
@@ -1161,21 +1164,42 @@ def _to_host_of(args, kwargs) -> None:
     visit(args)
     if kwargs:
         visit(tuple(kwargs.values()))
+    return found
+
+
+def _host_function(func, args, kwargs):
+    """HostParameter / HostTensor __torch_function__: metadata queries pass through; anything
+    else first brings the arenas of its lazy host arguments up to date from HBM, runs on the
+    plain tensors, and reports every argument it wrote (its version counter moved) to its
+    mirror, which uploads that arena before the next outer-step call."""
+    kwargs = kwargs or {}
+    if func in _META:
+        with _NO_TF():
+            return func(*args, **kwargs)
+    found = _host_args(args, kwargs)
+    with _NO_TF():
+        vers = [x._version for x, _, _ in found]
+        out = func(*args, **kwargs)
+        for (x, m, arena), v in zip(found, vers):
+            if x._version != v:
+                m.host_written(arena)
+    return out
+
+
+def _to_host_of(args, kwargs) -> None:
+    _host_args(args, kwargs)
 
 
 class HostTensor(torch.Tensor):
     """`.grad` or `outer_optimizer.state[p]["momentum_buffer"]` of the host-placed outer model
     under write_back="lazy": a CPU tensor (a view of a pinned host arena) whose values are
     copied from HBM the first time anything reads them after the device changed them -- any
-    torch function other than a metadata query, pickling, deep copy. Results of operations are
-    plain tensors."""
+    torch function other than a metadata query, pickling, deep copy -- and whose writes are
+    uploaded before the next outer-step call. Results of operations are plain tensors."""
 
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
-        if func not in _META:
-            _to_host_of(args, kwargs)
-        with _NO_TF():
-            return func(*args, **(kwargs or {}))
+        return _host_function(func, args, kwargs)
 
     def _plain(self) -> torch.Tensor:
         _to_host_of((self,), None)
@@ -1200,14 +1224,13 @@ class HostParameter(torch.nn.Parameter):
     so the optimizer's references stay valid -- holds a view of a pinned host arena that is
     brought up to date from HBM when it is read: any torch function on it other than a metadata
     query, `.data`, `.grad`, pickling, deep copy. Writes (in place, through `.data`, assigning
-    `.data` or `.grad`) are uploaded before the next outer-step call."""
+    `.data` or `.grad`) are uploaded before the next outer-step call. Writes through a `.data`
+    alias kept from earlier bypass every version counter: call invalidate() after them (as for
+    every placement)."""
 
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
-        if func not in _META:
-            _to_host_of(args, kwargs)
-        with _NO_TF():
-            return func(*args, **(kwargs or {}))
+        return _host_function(func, args, kwargs)
 
     def _m(self):
         r = self.__dict__.get("_dl_mirror")
@@ -1325,6 +1348,7 @@ class LazyHostOuterMirror:
         self._ver = {"theta": self.h["theta"]._version, "grad": self.h["grad"]._version,
                      "mom": None}
         self._dirty: set = set()
+        self._written: set = set()  # arenas written on the host since the last upload
         self._grads_set = False  # the API .grads are the grad arena's views
         self.theta_touched = self.grads_touched = False
 
@@ -1368,12 +1392,22 @@ class LazyHostOuterMirror:
             self.to_host(a)
 
     def invalidate(self) -> None:
+        """After writes the hooks cannot see (through a `.data` alias kept from earlier):
+        re-upload every host arena at the next call."""
         self.dev.invalidate()
         self.theta_touched = self.grads_touched = True
+        self._written |= {"theta", "grad", "mom"}
+
+    def host_written(self, arena: str) -> None:
+        self._written.add(arena)
 
     def _changed(self, arena: str, what: str) -> bool:
         h = self.h[arena]
-        if h is None or h._version == self._ver[arena]:
+        if h is None:
+            return False
+        if arena in self._written:
+            self._written.discard(arena)
+        elif h._version == self._ver[arena]:
             return False
         if arena in self._dirty:
             raise RuntimeError(

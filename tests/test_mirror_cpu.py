@@ -483,3 +483,22 @@ def test_boolean_knobs_parse_strictly(monkeypatch):
     monkeypatch.setenv("DILOCO_OUTER_FUSED", "off")
     outer = get_outer_model(inner, placement="device")
     assert not outer._diloco_mirror.fused
+
+
+def test_stock_torch_sgd_on_the_lazy_host_model():
+    """A stock torch.optim.SGD stepping the default (lazy host) outer model: it reads .grad
+    (the pending delta computed and copied first) and updates the CPU parameters in place;
+    those writes -- on the Parameter objects, whose version counters are their own -- must reach
+    the HBM twin before sync_inner_model writes the inner parameters. Two outer steps bit-exact
+    vs the reference."""
+    g = load_npz("micro_n1.npz")
+    inner, outer = _models(None)
+    opt = torch.optim.SGD(outer.parameters(), lr=0.7, momentum=0.9, nesterov=True)
+    for s in (1, 2):
+        _set_inner(inner, outer, s)
+        compute_pseudo_gradient(inner, outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        assert _host(outer.parameters()).tobytes() == g[f"theta_s{s}"].tobytes(), s
+        assert _host(inner.parameters()).tobytes() == g[f"theta_s{s}"].tobytes(), s
+        assert _host(p.grad for p in outer.parameters()).tobytes() == g[f"delta_s{s}_r0"].tobytes()
