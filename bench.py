@@ -1359,13 +1359,19 @@ def main():
                 exch[spec.name] = e
             if es is not None:
                 ks = max(3, a.steps // 4)
-                r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1)
+                # the 1.3B legs at N > 1 keep the outer model in HBM: the host placement's CPU
+                # copy (θ, .grad, momentum: 15.8 GB of host memory per rank, as the
+                # reference's own CPU outer model) times eight ranks is what a node's RAM holds
+                # only if nothing else does; the kernels and the exchange are the same
+                r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1, "f32", None,
+                          "sharded", False, False, "device")
                 ref13 = leg(f"rccl_ref_{es.name}", rccl_reference, dev, ws, rank,
                             es.total() // (64 * ws) * (64 * ws), 3, into=em.detail)
                 e = exchange_efficiency(r13, ref13, ws)
                 if e:
                     exch[es.name] = e
-                leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16")
+                leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16", None,
+                    "sharded", False, False, "device")
                 leg(f"{es.name}_int8", run_q8, es, dev, ws, rank, ks, 1, cap)
             leg(f"{spec.name}_grad_sync", gradsync_rate, spec, dev, ws, rank, max(3, a.steps // 2))
             if ws >= 4 and ws % 2 == 0:
