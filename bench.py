@@ -155,6 +155,9 @@ def dropin_bpp(ws, exchange, wire="f32"):
     return 12 + 20.0 / ws + 8
 
 
+_COMM: dict = {}
+
+
 def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange, placement=None):
     """The objects src/train.py builds for the outer step (train.py:375-421): an inner model on
     the GPU, get_outer_model(inner) -- by default the reference's host placement, stepped on an
@@ -186,7 +189,10 @@ def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange, placement=Non
             else:
                 os.environ[knob] = prev
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
-    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    if "comm" not in _COMM:  # one TrainingComm per run, as src/train.py:291 makes (its DP group
+        # -- an RCCL communicator at N > 1 -- is created once and shared by every leg)
+        _COMM["comm"] = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    comm = _COMM["comm"]
     # inner = θ_0 + this rank's noise (H inner steps' stand-in); later steps see inner = θ
     synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
                             out=[p.data.view(-1) for p in inner.parameters()])
