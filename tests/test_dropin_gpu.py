@@ -730,11 +730,14 @@ def test_serializer_errors_and_large_payload():
     assert torch.equal(yb[1], xb.float())
 
 
-def test_t125_fused_device_dropin_bit_exact_vs_oracle():
+@pytest.mark.parametrize("placement", ["device", None])
+def test_t125_fused_device_dropin_bit_exact_vs_oracle(placement):
     """The reference's four calls at full T125 size (148 tensors, 124,475,904 params) on the
-    fused device outer model, nothing read in between: each outer step is one
+    fused device outer model, and on the default outer model (the CPU outer model stepped on
+    its HBM twin, write_back="lazy"), nothing read in between: each outer step is one
     dl_delta_pack_sgd and sync_inner_model a verified no-op. θ, momentum, .grad and the inner
-    params bit-exact vs the C oracle on every tensor after each of 2 outer steps."""
+    params bit-exact vs the C oracle on every tensor after each of 2 outer steps (for the
+    default placement: read on the CPU, i.e. after the lazy copies from HBM)."""
     from diloco_amd import synth
     from diloco_amd.comm import TrainingComm
     from diloco_amd.trees import get_tree
@@ -750,14 +753,15 @@ def test_t125_fused_device_dropin_bit_exact_vs_oracle():
     inner.ps = torch.nn.ParameterList(
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, "cuda:0"),
                                                        shapes)])
-    outer = get_outer_model(inner, "device")
+    outer = get_outer_model(inner, placement)
     assert outer._diloco_mirror.fused
+    assert all(p.device.type == ("cuda" if placement else "cpu") for p in outer.parameters())
     opt = get_optimizer(outer, SGD_CFG)
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     st = oracle.OuterState([p.detach().cpu().numpy().reshape(-1) for p in outer.parameters()])
     for s in (1, 2):
-        synth.inner_tree_device([p.detach().view(-1) for p in outer.parameters()], s, 0,
-                                out=[p.data.view(-1) for p in inner.parameters()])
+        synth.inner_tree_device([p.detach().view(-1).to("cuda:0") for p in outer.parameters()],
+                                s, 0, out=[p.data.view(-1) for p in inner.parameters()])
         compute_pseudo_gradient(inner, outer)
         comm.sync_gradients(outer)
         opt.step()
