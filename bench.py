@@ -1353,22 +1353,14 @@ def main():
                 None, "sharded", False, True)
             leg("dropin_pcie", dropin_pcie, spec, dev, ws, rank, 5)
         else:
-            for ex in ("replicated", "a2a"):
-                leg(f"{spec.name}_dropin_{ex}", run_dropin, spec, dev, ws, rank, a.steps,
-                    a.warmup, "f32", None, ex)
-            leg(f"{spec.name}_engine", run_engine, spec, dev, ws, rank, a.steps, a.warmup,
-                torch.float32, cap)
-            ref = leg(f"rccl_ref_{spec.name}", rccl_reference, dev, ws, rank,
-                      head["padded"] // (64 * ws) * (64 * ws), into=em.detail)
-            e = exchange_efficiency(head, ref, ws)
-            if e:
-                exch[spec.name] = e
             if es is not None:
+                # first: the north star's N > 1 figure -- the 1.3B bucket set through the calls
+                # against RCCL's own all_reduce of the same bytes, this node, this run
                 ks = max(3, a.steps // 4)
                 # the 1.3B legs at N > 1 keep the outer model in HBM: the host placement's CPU
                 # copy (θ, .grad, momentum: 15.8 GB of host memory per rank, as the
-                # reference's own CPU outer model) times eight ranks is what a node's RAM holds
-                # only if nothing else does; the kernels and the exchange are the same
+                # reference's own CPU outer model) times eight ranks is what a node's RAM
+                # holds only if nothing else does; the kernels and the exchange are the same
                 r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1, "f32", None,
                           "sharded", False, False, "device")
                 ref13 = leg(f"rccl_ref_{es.name}", rccl_reference, dev, ws, rank,
@@ -1376,6 +1368,17 @@ def main():
                 e = exchange_efficiency(r13, ref13, ws)
                 if e:
                     exch[es.name] = e
+            ref = leg(f"rccl_ref_{spec.name}", rccl_reference, dev, ws, rank,
+                      head["padded"] // (64 * ws) * (64 * ws), into=em.detail)
+            e = exchange_efficiency(head, ref, ws)
+            if e:
+                exch[spec.name] = e
+            for ex in ("replicated", "a2a"):
+                leg(f"{spec.name}_dropin_{ex}", run_dropin, spec, dev, ws, rank, a.steps,
+                    a.warmup, "f32", None, ex)
+            leg(f"{spec.name}_engine", run_engine, spec, dev, ws, rank, a.steps, a.warmup,
+                torch.float32, cap)
+            if es is not None:
                 leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16", None,
                     "sharded", False, False, "device")
                 leg(f"{es.name}_int8", run_q8, es, dev, ws, rank, ks, 1, cap)
