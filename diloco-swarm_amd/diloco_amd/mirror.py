@@ -461,8 +461,10 @@ class OuterParameter(torch.nn.Parameter):
             m.theta_touched = True
         _DATA.__set__(self, value)
 
-    def __reduce_ex__(self, proto):  # pickles as a plain Parameter (the mirror stays behind)
-        return (torch._utils._rebuild_parameter, (self.data, self.requires_grad, OrderedDict()))
+    def __reduce_ex__(self, proto):  # pickles as a plain Parameter (the mirror stays behind),
+        # over its own storage (a view would carry the whole packed arena)
+        return (torch._utils._rebuild_parameter,
+                (_DATA.__get__(self).clone(), self.requires_grad, OrderedDict()))
 
     def __deepcopy__(self, memo):  # ... and deep-copies as one (a clone of the values)
         if id(self) in memo:
@@ -1279,8 +1281,10 @@ class HostParameter(torch.nn.Parameter):
         with _NO_TF():
             _GRAD.__delete__(self)
 
-    def __reduce_ex__(self, proto):  # pickles as a plain Parameter of the current values
-        return (torch._utils._rebuild_parameter, (self.data, self.requires_grad, OrderedDict()))
+    def __reduce_ex__(self, proto):  # pickles as a plain Parameter of the current values,
+        # over its own storage (a view would carry the whole pinned arena)
+        return (torch._utils._rebuild_parameter,
+                (self.data.clone(), self.requires_grad, OrderedDict()))
 
     def __deepcopy__(self, memo):
         if id(self) in memo:
