@@ -198,14 +198,16 @@ def _worker(rank, world, port, mode, out):
                             world_size=world)
     rec = {}
     if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_device_quiet",
-                "dropin_device_bf16", "dropin_device_quiet_buckets"):
-        if mode == "dropin_device_quiet_buckets":  # several buckets: the SGD pass of bucket b
+                "dropin_device_bf16", "dropin_device_quiet_buckets", "dropin_quiet_buckets",
+                "dropin_sync"):
+        if mode.endswith("_quiet_buckets"):  # several buckets: the SGD pass of bucket b
             os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # waits for b's collective only
         rec = _outer_steps(rank, world,
                            placement="device" if mode.startswith("dropin_device") else None,
-                           write_back="deferred" if mode == "dropin_deferred" else None,
+                           write_back="deferred" if mode == "dropin_deferred" else
+                           "sync" if mode == "dropin_sync" else None,
                            quiet=mode in ("dropin_device_quiet", "dropin_device_bf16",
-                                          "dropin_device_quiet_buckets"),
+                                          "dropin_device_quiet_buckets", "dropin_quiet_buckets"),
                            wire="bf16" if mode == "dropin_device_bf16" else None)
     elif mode in ("engine", "engine_ar"):
         from diloco_amd import synth
@@ -517,9 +519,13 @@ def _run(mode, world=2):  # noqa: D401
 
 
 @pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_device_quiet",
-                                  "dropin_device_quiet_buckets", "dropin_deferred", "engine",
-                                  "engine_ar"])
+                                  "dropin_device_quiet_buckets", "dropin_quiet_buckets",
+                                  "dropin_sync", "dropin_deferred", "engine", "engine_ar"])
 def test_two_peers_on_gpu_match_reference(mode):
+    """Two processes on the GPU, gloo DP group: dropin / dropin_quiet_buckets = the default
+    placement (the CPU outer model on its HBM twin; the sharded exchange, several buckets in
+    flight), dropin_sync / dropin_deferred = host-authoritative write-backs, dropin_device* =
+    the outer model in HBM; every value bit-exact vs the reference's 2-peer run."""
     g = load_npz("micro_n2.npz")
     for rec in _run(mode):
         for s in (1, 2):
