@@ -147,6 +147,9 @@ def dropin_bpp(ws, exchange, wire="f32"):
     dl_unpack_sgd with the inner write 24 (bf16 wire 22)."""
     if ws == 1:
         return 28.0
+    if wire == "int8":  # dl_delta_q8 8 + slot, dl_q8_reduce (n + 1)/n slots, dl_unpack_sgd_q8
+        sb = 4160.0 / 4096  # one 4160-B slot per 4096-element chunk
+        return 8 + sb + (ws + 1) * sb / ws + sb + 24.0
     wb = 2 if wire == "bf16" else 4
     if wire == "bf16" or exchange == "replicated":
         return 8 + wb + wb + 20.0
@@ -236,7 +239,8 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
     P = spec.total()
     mm = outer._diloco_mirror
     m = getattr(mm, "dev", mm)  # the lazy host placement steps on its HBM twin
-    ex = "replicated" if wire == "bf16" else m.exchange  # the bf16 wire: RCCL's bf16 all_reduce
+    # the bf16 wire: RCCL's bf16 all_reduce; int8: its all_to_all + rank-order reduce
+    ex = "replicated" if wire == "bf16" else "int8 a2a" if wire == "int8" else m.exchange
     bpp = dropin_bpp(ws, ex, wire)
     res = {"tree": spec.name, "params": P, "tensors": len(m.params), "padded": m.tree.total,
            "buckets": m.tree.n_buckets, "ms_per_step": dt * 1e3, "value": 4.0 * P / dt / 1e9,
@@ -279,6 +283,31 @@ def exchange_roofline(m, ws, dev, steps, group):
     (n-1)/n of the wire + (n-1)/n of θ for the sharded forms, 2(n-1)/n of the wire for the
     all-reduce; peak (n-1) x 153 GB/s (one xGMI link per peer)."""
     rank = dist.get_rank(group)
+    if m.wire == "int8":  # all_to_all + all_gather of every bucket's slots
+        q = m._q8
+        S = q["S"]
+        recv = q["recv"][0]
+        slot_bytes = sum(q["n"] * p[1] for p in q["plan"]) * S
+
+        def once_q8():
+            for b, (nch, mm, base, rb) in enumerate(q["plan"]):
+                region = m._q8_region(q, b)
+                dist.all_to_all_single(recv[:ws * mm * S], region, group=group)
+                dist.all_gather_into_tensor(region, q["red"][rb * S:(rb + mm) * S], group=group)
+
+        once_q8()
+        _sync(ws)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = max(3, steps // 2)
+        e0.record()
+        for _ in range(reps):
+            once_q8()
+        e1.record()
+        e1.synchronize()
+        ms = _max_over_ranks(e0.elapsed_time(e1) / reps, dev, ws)
+        return kernel_entry(2.0 * (ws - 1) / ws * slot_bytes, ms, bound="xgmi",
+                            peak=(ws - 1) * XGMI_LINK_GBS,
+                            kernel="rccl all_to_all + all_gather of the int8 slots")
     w = m.d_wire16 if m.wire == "bf16" else m.d_wire
     sharded = m.exchange != "replicated" and m.wire != "bf16"
     recv = torch.empty_like(w) if m.exchange == "a2a" else None
@@ -1381,7 +1410,8 @@ def main():
             if es is not None:
                 leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16", None,
                     "sharded", False, False, "device")
-                leg(f"{es.name}_int8", run_q8, es, dev, ws, rank, ks, 1, cap)
+                leg(f"{es.name}_dropin_int8", run_dropin, es, dev, ws, rank, ks, 1, "int8", None,
+                    "sharded", False, False, "device")
             leg(f"{spec.name}_grad_sync", gradsync_rate, spec, dev, ws, rank, max(3, a.steps // 2))
             if ws >= 4 and ws % 2 == 0:
                 leg(f"{spec.name}_two_stages", run_two_stages, spec, dev, ws, rank, a.steps,

@@ -44,6 +44,7 @@ from .outer import pipelined_buckets
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_GRAD, SLOT_INNER
 
 ALL = _lib.ALL_BUCKETS
+S_CHUNK = _lib.CHUNK_ELEMS  # elements per tree chunk (one int8 slot each)
 
 
 def _check_host_params(params: Sequence[torch.Tensor]) -> None:
@@ -56,7 +57,7 @@ def _check_host_params(params: Sequence[torch.Tensor]) -> None:
 
 
 WRITE_BACKS = ("lazy", "sync", "deferred")
-OUTER_WIRES = ("f32", "bf16")
+OUTER_WIRES = ("f32", "bf16", "int8")
 # The DP exchange behind sync_gradients for the device outer model at N > 1:
 #   "sharded"     per bucket RCCL reduce_scatter -> Nesterov SGD on this rank's 1/n of θ and
 #                 the momentum -> RCCL all_gather of θ (20 + 20/n B/param of HBM)
@@ -868,7 +869,9 @@ class DeviceOuterMirror:
         if self._delta is not None:
             self._take_delta()
             self.k.delta_pack(self.tree, ALL, SLOT_INNER, self.d_theta, self.d_wire)
-        if self._xmode is not None:  # sharded: a collective over the DP group (see class doc)
+        if self._xmode == "q8":  # the averaged int8 slots, decoded into .grad's arena
+            self._decode_q8()
+        elif self._xmode is not None:  # sharded: a collective over the DP group (class doc)
             self._gather_wire()
         if self._sum16:  # bf16 wire: the decoded average (/n in fp32) into .grad's arena
             div, self._div, self._sum16 = self._div, 1, False
@@ -916,6 +919,9 @@ class DeviceOuterMirror:
                    ordered: bool = False) -> None:
         """grad = Σ_peers grad / n (src/comm.py:120-123), in place on the packed .grad.
         ordered (DILOCO_DP_EXCHANGE=a2a): the rank-order sum, bit-exact at every n."""
+        if self.wire == "int8":  # its exchange sums in rank order already (dl_q8_reduce)
+            self._all_reduce_q8(group, num_peers)
+            return
         mode = self._exchange_mode(num_peers, ordered)
         if self.wire == "bf16":
             self._all_reduce_bf16(group, num_peers)
@@ -1028,6 +1034,125 @@ class DeviceOuterMirror:
         self._xmode, self._xgroup, self._xn, self._xrank = mode, group, n, rank
         self._div = n if mode == "sharded" else 1
 
+    # ---- the int8 wire behind the reference's calls ------------------------
+    def _q8_buffers(self, n: int) -> dict:
+        """Slot regions of every bucket (n·m slots of Q8_SLOT bytes: the bucket's chunks in
+        order, zero padding to a multiple of n), two all_to_all landing buffers, one reduced
+        region per bucket (so every bucket's all_gather may stay in flight)."""
+        q = getattr(self, "_q8", None)
+        if q is not None and q["n"] == n:
+            return q
+        from .kernels import Q8_SLOT
+
+        plan, base, rbase, mmax = [], 0, 0, 1
+        for c0, c1 in self.tree.bucket_chunks:
+            m = max(1, -(-(c1 - c0) // n))
+            plan.append((c1 - c0, m, base, rbase))
+            base += n * m
+            rbase += m
+            mmax = max(mmax, m)
+        z = dict(dtype=torch.uint8, device=self.device)
+        segs = []
+        for lo, hi in self.tree.bucket_ranges:
+            segs.append([i for i, o in enumerate(self.offs) if lo <= o < hi])
+        self._q8 = q = {"n": n, "plan": plan, "S": Q8_SLOT, "segs": segs,
+                        "slots": torch.zeros(base * Q8_SLOT, **z),
+                        "red": torch.zeros(rbase * Q8_SLOT, **z),
+                        "recv": [torch.zeros(n * mmax * Q8_SLOT, **z) for _ in range(2)]}
+        return q
+
+    def _q8_region(self, q: dict, b: int) -> torch.Tensor:
+        nch, m, base, _ = q["plan"][b]
+        return q["slots"][base * q["S"]:(base + q["n"] * m) * q["S"]]
+
+    def _all_reduce_q8(self, group, n: int) -> None:
+        """Per bucket: dl_delta_q8 (the pending delta quantised straight from θ and the inner
+        params; else .grad's fp32 arena) -> all_to_all -> dl_q8_reduce (Σ over the peers in rank
+        order, / n, re-quantised) -> all_gather of the averaged slots, left in flight (the
+        next bucket's pack and all_to_all are issued before this one's reduce). Fused: the SGD
+        pass dequantises inside dl_unpack_sgd_q8; .grad shows the decoded average when read.
+        Eager: decoded into .grad at once."""
+        if self._delta is not None:
+            self._take_delta()
+            self._relay_theta()
+            self._grad_views()
+            theta, slot = self.d_theta, SLOT_INNER
+        else:
+            if self.pending:
+                self.settle_grads()  # a second sync_gradients reduces the averages
+            self._relay_grads(zero_fill_missing=True)
+            # the deltas are .grad itself: quantise (wire - 0) -> θ slot holds the wire,
+            # the "inner" slot zeros (a zero arena bound in the auxiliary slot)
+            if getattr(self, "_q8_zero", None) is None:
+                self._q8_zero = [torch.zeros_like(v) for v in self._views["wire"]]
+                from .plan import SLOT_AUX
+                self.k.bind(self.tree, SLOT_AUX, self._q8_zero, self.device)
+            from .plan import SLOT_AUX
+            theta, slot = self.d_wire, SLOT_AUX
+        q = self._q8_buffers(n)
+        S, nb = q["S"], self.tree.n_buckets
+
+        def pack(b):
+            self.k.delta_q8(self.tree, b, slot, theta, self._q8_region(q, b))
+
+        def a2a(b):
+            nch, m, _, _ = q["plan"][b]
+            return dist.all_to_all_single(q["recv"][b % 2][:n * m * S], self._q8_region(q, b),
+                                          group=group, async_op=True)
+
+        works, pend = [None] * nb, [None] * nb
+        pack(0)
+        pend[0] = a2a(0)
+        for b in range(nb):
+            if b + 1 < nb:
+                pack(b + 1)
+                pend[b + 1] = a2a(b + 1)
+            pend[b].wait()
+            nch, m, _, rb = q["plan"][b]
+            red = q["red"][rb * S:(rb + m) * S]
+            self.k.q8_reduce(q["recv"][b % 2][:n * m * S], n, m, n, red)
+            works[b] = dist.all_gather_into_tensor(self._q8_region(q, b), red, group=group,
+                                                   async_op=True)
+        self._works = works
+        self._xmode, self._div = "q8", 1
+        if not self.fused:
+            self._decode_q8()
+
+    def _decode_q8(self) -> None:
+        """The averaged slots -> .grad's fp32 arena: g = q · s per chunk (the product
+        dl_unpack_sgd_q8 forms in registers), chunk j of a tensor covering its elements
+        [4096·j, 4096·(j+1))."""
+        self._join()
+        self._xmode = None
+        q = self._q8
+        S, C = q["S"], S_CHUNK
+        for b in range(self.tree.n_buckets):
+            nch, m, base, _ = q["plan"][b]
+            sl = q["slots"][base * S:(base + nch) * S].view(nch, S)
+            g = sl[:, S - C:].contiguous().view(torch.int8).float() * \
+                sl[:, :4].contiguous().view(torch.float32)
+            r = 0
+            for i in q["segs"][b]:
+                n_i = self.numels[i]
+                k = -(-n_i // C)
+                self.d_wire[self.offs[i]:self.offs[i] + n_i].copy_(g[r:r + k].reshape(-1)[:n_i])
+                r += k
+
+    def _q8_sgd(self, mom, lr, momentum, nesterov, first, target) -> None:
+        """Per bucket: wait for its all_gather, then dl_unpack_sgd_q8 (g = q·s, Nesterov SGD
+        on θ and the momentum, the inner params written when the last delta's are bound)."""
+        works, self._works = self._works, None
+        q = self._q8
+        write = target is not None
+        if write:
+            self.k.bind(self.tree, SLOT_INNER, target[0], self.device, key=tuple(target[1]))
+        for b in range(self.tree.n_buckets):
+            if works is not None:
+                works[b].wait()
+            self.k.unpack_sgd_q8(self.tree, b, self._q8_region(q, b), self.d_theta, mom, lr,
+                                 momentum, nesterov, first, SLOT_INNER if write else -1)
+        # the slots keep the average for a later .grad read (_xmode stays "q8")
+
     def _launch_reductions(self, pack, view, group) -> None:
         """Fused N > 1: pack(b) then an asynchronous all_reduce(SUM) of bucket b, for every
         bucket, none waited for here (OuterSGD.step waits bucket by bucket, anything that reads
@@ -1080,7 +1205,8 @@ class DeviceOuterMirror:
                 first = False  # the buffers this mirror returned last step
             self._mom_src = bufs
         mom = self.d_mom if momentum != 0 else None
-        sharded = delta is None and self._xmode is not None
+        sharded = delta is None and self._xmode in ("sharded", "a2a")
+        q8 = delta is None and self._xmode == "q8"
         if (mom is not None and self._mom_stale and not first
                 and not (sharded and self._mom_shard == (self._xgroup, self._xn, self._xrank))):
             self.gather_momentum()  # a whole-tree update needs every slice of the momentum
@@ -1095,6 +1221,9 @@ class DeviceOuterMirror:
             self._mom_stale = False
         elif sharded:  # N > 1, sharded exchange: this rank's 1/n, then all_gather(θ)
             self._sharded_sgd(mom, lr, momentum, nesterov, first, target)
+        elif q8:  # N > 1, int8 wire: the averaged slots of each bucket, SGD fused in
+            self._mom_stale = False
+            self._q8_sgd(mom, lr, momentum, nesterov, first, target)
         else:
             self._mom_stale = False
             if write:

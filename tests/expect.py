@@ -26,6 +26,8 @@ def expected_q8(n, steps=2, cap=MICRO_Q8_CAP):
         for t in range(len(theta)):
             oracle.sgd(theta[t], buf[t], g[t], 0.7, 0.9, True, s == 1)
         out[f"theta_s{s}"] = np.concatenate(theta)
+        out[f"buf_s{s}"] = np.concatenate(buf)
+        out[f"avg_s{s}"] = np.concatenate(g)
     return out
 
 

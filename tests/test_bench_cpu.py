@@ -128,7 +128,7 @@ def _full_run_records(ws):
            "roofline": dict(roof, note="y" * 500), "kernels": {"a": roof, "b": roof},
            "hbm_bytes_per_param": 22.5, "variant": "z" * 300}
     names = ([f"t125_dropin_{e}" for e in ("replicated", "a2a")] +
-             ["t125_engine", "t1.3b_dropin", "t1.3b_dropin_bf16", "t1.3b_int8",
+             ["t125_engine", "t1.3b_dropin", "t1.3b_dropin_bf16", "t1.3b_int8", "t1.3b_dropin_int8",
               "t125_grad_sync", "t125_two_stages", "xgmi_link_probe", "t1.3b_xgmi_inner",
               "t125_dropin_synced", "dropin_pcie", "t1.3b_bf16"])
     legs = {n: dict(rec) for n in names}

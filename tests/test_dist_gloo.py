@@ -77,9 +77,11 @@ def _worker(rank, world, port, mode, num_stages, out):
                 "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
                 "dropin_device_a2a_dp", "dropin_a2a_dp", "dropin_device_momentum_first",
                 "dropin_device_eager_a2a_dp", "dropin_sync", "dropin_sync_a2a_dp",
-                "dropin_quiet"):
+                "dropin_quiet", "dropin_device_int8", "dropin_device_int8_eager",
+                "dropin_int8"):
         if mode in ("dropin_device_quiet_buckets", "dropin_device_quiet_a2a",
-                    "dropin_device_momentum_first"):  # the exchange in several buckets: the
+                    "dropin_device_momentum_first", "dropin_device_int8",
+                    "dropin_device_int8_eager", "dropin_int8"):  # several buckets: the
             os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # SGD waits bucket by bucket
         if mode.endswith("_a2a_dp"):  # DILOCO_DP_EXCHANGE=a2a behind sync_gradients
             import diloco_amd.comm as comm_mod
@@ -97,13 +99,15 @@ def _worker(rank, world, port, mode, num_stages, out):
         # so the fused device model defers the delta and the /n into its one SGD pass
         quiet = mode in ("dropin_device_quiet", "dropin_device_bf16", "dropin_device_quiet_buckets",
                          "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
-                         "dropin_device_a2a_dp", "dropin_device_momentum_first", "dropin_quiet")
+                         "dropin_device_a2a_dp", "dropin_device_momentum_first", "dropin_quiet",
+                         "dropin_device_int8")
         device = mode.startswith("dropin_device")
         inner = _micro_module(theta0, shapes)
         outer = get_outer_model(inner, placement="device" if device else None,
                                 write_back="deferred" if deferred else "sync" if sync else None,
                                 fused="_eager" not in mode,
-                                wire="bf16" if "bf16" in mode else None, exchange=exchange)
+                                wire="bf16" if "bf16" in mode else "int8" if "int8" in mode
+                                else None, exchange=exchange)
         opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
         assert type(opt).__name__ == "OuterSGD"
         from diloco_amd.utils import outer_mirror
@@ -528,6 +532,24 @@ def test_dropin_device_bf16_wire_two_peers(mode):
     exp = expected_bf16_allreduce(2)
     recs = _run(mode, 2)
     for rec in recs:
+        for s in (1, 2):
+            for k in ("theta", "buf", "avg"):
+                assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (mode, k, s)
+            assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), (mode, s)
+
+
+@pytest.mark.parametrize("mode", ["dropin_device_int8", "dropin_device_int8_eager",
+                                  "dropin_int8"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_dropin_int8_wire_matches_codec_restatement(mode, world):
+    """The int8 wire behind the reference's calls (get_outer_model(..., wire="int8"), SURVEY
+    §8f row 4): per bucket dl_delta_q8 -> all_to_all -> dl_q8_reduce (rank order) ->
+    all_gather, the SGD reading the averaged slots (fused) or the decoded .grad (eager); the
+    device placement and the default host placement. .grad (the decoded average), θ, the
+    momentum and the inner params bit-identical to the oracle's restatement of the codec
+    (tests/expect.expected_q8) at 2 and 4 peers, in several buckets."""
+    exp = expected_q8(world)
+    for rec in _run(mode, world):
         for s in (1, 2):
             for k in ("theta", "buf", "avg"):
                 assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (mode, k, s)

@@ -199,16 +199,18 @@ def _worker(rank, world, port, mode, out):
     rec = {}
     if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_device_quiet",
                 "dropin_device_bf16", "dropin_device_quiet_buckets", "dropin_quiet_buckets",
-                "dropin_sync"):
-        if mode.endswith("_quiet_buckets"):  # several buckets: the SGD pass of bucket b
+                "dropin_sync", "dropin_device_int8", "dropin_int8"):
+        if mode.endswith("_quiet_buckets") or "int8" in mode:  # several buckets: bucket b's
             os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # waits for b's collective only
         rec = _outer_steps(rank, world,
                            placement="device" if mode.startswith("dropin_device") else None,
                            write_back="deferred" if mode == "dropin_deferred" else
                            "sync" if mode == "dropin_sync" else None,
                            quiet=mode in ("dropin_device_quiet", "dropin_device_bf16",
-                                          "dropin_device_quiet_buckets", "dropin_quiet_buckets"),
-                           wire="bf16" if mode == "dropin_device_bf16" else None)
+                                          "dropin_device_quiet_buckets", "dropin_quiet_buckets",
+                                          "dropin_device_int8"),
+                           wire="bf16" if mode == "dropin_device_bf16" else
+                           "int8" if "int8" in mode else None)
     elif mode in ("engine", "engine_ar"):
         from diloco_amd import synth
         from diloco_amd.outer import OuterSync
@@ -886,3 +888,20 @@ def test_outer_model_deepcopies_and_pickles_with_the_hip_library(placement):
     bio.seek(0)
     st = torch.load(bio, weights_only=True)["state"]
     assert _flat(st[i]["momentum_buffer"] for i in range(len(st))).tobytes() == g["buf_s1"].tobytes()
+
+
+@pytest.mark.parametrize("mode", ["dropin_device_int8", "dropin_int8"])
+def test_dropin_int8_wire_two_peers_on_gpu(mode):
+    """The int8 wire behind the reference's calls on the GPU (two processes, gloo DP group,
+    several buckets): the device placement with nothing read between the calls (the SGD reads
+    the averaged slots, dl_unpack_sgd_q8) and the default host placement read after every
+    call (the slots decoded into .grad). .grad, θ, momentum and the inner params bit-exact vs
+    the oracle's restatement of the codec (tests/expect.expected_q8)."""
+    from expect import expected_q8
+
+    exp = expected_q8(2)
+    for rec in _run(mode):
+        for s in (1, 2):
+            for k in ("theta", "buf", "avg"):
+                assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (mode, k, s)
+            assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), (mode, s)
