@@ -502,3 +502,39 @@ def test_stock_torch_sgd_on_the_lazy_host_model():
         assert _host(outer.parameters()).tobytes() == g[f"theta_s{s}"].tobytes(), s
         assert _host(inner.parameters()).tobytes() == g[f"theta_s{s}"].tobytes(), s
         assert _host(p.grad for p in outer.parameters()).tobytes() == g[f"delta_s{s}_r0"].tobytes()
+
+
+@pytest.mark.parametrize("placement", [None, "device"])
+def test_checkpoint_resume_through_state_dicts(placement):
+    """Resume as a training script would: after outer step 1 save the outer model's and the
+    outer optimizer's state_dicts, build a fresh outer model + OuterSGD (the default lazy host
+    placement, and the device placement), load both, run outer step 2: θ, the momentum,
+    .grad and the inner params equal the reference's uninterrupted step 2 (micro_n1.npz)."""
+    import io
+
+    g = load_npz("micro_n1.npz")
+    inner, outer = (_models(None) if placement is None else _device_models(True))
+    opt = get_optimizer(outer, SGD_CFG)
+    _set_inner(inner, outer, 1)
+    compute_pseudo_gradient(inner, outer)
+    opt.step()
+    sync_inner_model(outer, inner)
+    bio = io.BytesIO()
+    torch.save({"model": outer.state_dict(), "opt": opt.state_dict()}, bio)
+    bio.seek(0)
+    ck = torch.load(bio, weights_only=True)
+    # a fresh outer model from a fresh inner model (θ_0), then the checkpoint loaded into both
+    inner2, outer2 = (_models(None) if placement is None else _device_models(True))
+    opt2 = get_optimizer(outer2, SGD_CFG)
+    outer2.load_state_dict(ck["model"])
+    opt2.load_state_dict(ck["opt"])
+    sync_inner_model(outer2, inner2)  # the inner model starts from the loaded θ
+    _set_inner(inner2, outer2, 2)
+    compute_pseudo_gradient(inner2, outer2)
+    opt2.step()
+    sync_inner_model(outer2, inner2)
+    assert _host(outer2.parameters()).tobytes() == g["theta_s2"].tobytes()
+    assert _host(opt2.state[p]["momentum_buffer"]
+                 for p in outer2.parameters()).tobytes() == g["buf_s2"].tobytes()
+    assert _host(p.grad for p in outer2.parameters()).tobytes() == g["delta_s2_r0"].tobytes()
+    assert _host(inner2.parameters()).tobytes() == g["theta_s2"].tobytes()
