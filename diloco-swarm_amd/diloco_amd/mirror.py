@@ -1461,7 +1461,11 @@ class LazyHostOuterMirror:
         self._twin = twin
         self.fused, self.wire, self.exchange = fused, wire, exchange
         self.tree, self.offs, self.numels = self.dev.tree, self.dev.offs, self.dev.numels
-        pin = self.device.type == "cuda"
+        # the host arenas are pinned by default (one async DMA per read); DILOCO_LAZY_PIN=0
+        # keeps them pageable (plain memcpy-staged copies on read; no page-locked memory)
+        import os
+
+        pin = self.device.type == "cuda" and os.environ.get("DILOCO_LAZY_PIN", "1") != "0"
         z = dict(dtype=torch.float32, pin_memory=pin)
         self.h = {"theta": torch.zeros(self.tree.total, **z),
                   "grad": torch.zeros(self.tree.total, **z), "mom": None}
