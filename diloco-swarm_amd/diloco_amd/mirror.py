@@ -594,8 +594,24 @@ class DeviceOuterMirror:
         self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems, dp_bucket_align())
         self.offs = [int(o) for o in self.tree.seg_off[:-1]]
         z = dict(dtype=torch.float32, device=self.device)
-        self.d_theta = torch.zeros(self.tree.total, **z)
-        self.d_wire = torch.zeros(self.tree.total, **z)
+        import os
+
+        self._mom_arena: Optional[torch.Tensor] = None
+        if os.environ.get("DILOCO_ONE_ARENA") == "1":
+            # θ, the wire and the momentum carved out of ONE allocation (A/B knob,
+            # tools/placement_ab.py): three tensors over one storage, each with its own
+            # version counter (set_ on a fresh tensor), zero-initialised
+            st = torch.zeros(3 * self.tree.total, **z).untyped_storage()
+
+            def carve(i):
+                t = torch.empty(0, **z)
+                t.set_(st, i * self.tree.total, (self.tree.total,))
+                return t
+
+            self.d_theta, self.d_wire, self._mom_arena = carve(0), carve(1), carve(2)
+        else:
+            self.d_theta = torch.zeros(self.tree.total, **z)
+            self.d_wire = torch.zeros(self.tree.total, **z)
         self.d_mom: Optional[torch.Tensor] = None
         # wire="bf16" (BASELINE config #5 behind the drop-in calls): at N > 1 the deltas cross
         # the wire in bf16 (cast in the pack kernel, RCCL's bf16 SUM) and the SGD pass reads
@@ -1178,7 +1194,8 @@ class DeviceOuterMirror:
         bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
         if momentum != 0:
             if self.d_mom is None:
-                self.d_mom = torch.zeros_like(self.d_theta)
+                self.d_mom = (self._mom_arena if self._mom_arena is not None
+                              else torch.zeros_like(self.d_theta))
                 plain = self._make_views(self.d_mom)
                 self._views["mom_plain"] = plain
                 self._views["mom"] = [self._momentum_buffer(v) for v in plain]

@@ -51,10 +51,11 @@ def main():
     setups = {}
     for name in order:
         os.environ["DILOCO_LAZY_PIN"] = "0" if name == "lazy_nopin" else "1"
+        os.environ["DILOCO_ONE_ARENA"] = "1" if name.endswith("_one") else "0"
         inner = torch.nn.Module()
         inner.ps = torch.nn.ParameterList([torch.nn.Parameter(t.view(s)) for t, s in zip(
             synth.outer_tree_device(spec, dev), shapes)])
-        outer = get_outer_model(inner, "device" if name == "device" else None)
+        outer = get_outer_model(inner, "device" if name.startswith("device") else None)
         opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9,
                                                    nesterov=True))
         synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, 0,
