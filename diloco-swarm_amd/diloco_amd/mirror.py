@@ -594,24 +594,8 @@ class DeviceOuterMirror:
         self.tree = self.k.tree(self.numels, self.device, bucket_cap_elems, dp_bucket_align())
         self.offs = [int(o) for o in self.tree.seg_off[:-1]]
         z = dict(dtype=torch.float32, device=self.device)
-        import os
-
-        self._mom_arena: Optional[torch.Tensor] = None
-        if os.environ.get("DILOCO_ONE_ARENA") == "1":
-            # θ, the wire and the momentum carved out of ONE allocation (A/B knob,
-            # tools/placement_ab.py): three tensors over one storage, each with its own
-            # version counter (set_ on a fresh tensor), zero-initialised
-            st = torch.zeros(3 * self.tree.total, **z).untyped_storage()
-
-            def carve(i):
-                t = torch.empty(0, **z)
-                t.set_(st, i * self.tree.total, (self.tree.total,))
-                return t
-
-            self.d_theta, self.d_wire, self._mom_arena = carve(0), carve(1), carve(2)
-        else:
-            self.d_theta = torch.zeros(self.tree.total, **z)
-            self.d_wire = torch.zeros(self.tree.total, **z)
+        self.d_theta = torch.zeros(self.tree.total, **z)
+        self.d_wire = torch.zeros(self.tree.total, **z)
         self.d_mom: Optional[torch.Tensor] = None
         # wire="bf16" (BASELINE config #5 behind the drop-in calls): at N > 1 the deltas cross
         # the wire in bf16 (cast in the pack kernel, RCCL's bf16 SUM) and the SGD pass reads
@@ -1478,11 +1462,9 @@ class LazyHostOuterMirror:
         self._twin = twin
         self.fused, self.wire, self.exchange = fused, wire, exchange
         self.tree, self.offs, self.numels = self.dev.tree, self.dev.offs, self.dev.numels
-        # the host arenas are pinned by default (one async DMA per read); DILOCO_LAZY_PIN=0
-        # keeps them pageable (plain memcpy-staged copies on read; no page-locked memory)
-        import os
-
-        pin = self.device.type == "cuda" and os.environ.get("DILOCO_LAZY_PIN", "1") != "0"
+        # pinned host arenas: one async DMA per read (pageable arenas measured the same for the
+        # step itself, profiles/r04_placement_ab_order.txt)
+        pin = self.device.type == "cuda"
         z = dict(dtype=torch.float32, pin_memory=pin)
         self.h = {"theta": torch.zeros(self.tree.total, **z),
                   "grad": torch.zeros(self.tree.total, **z), "mom": None}

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Interleaved A/B of the drop-in step's placements on T125, one GPU: the default (the
 reference's CPU outer model stepped on its HBM twin, write_back="lazy", pinned host arenas),
-the same with pageable host arenas (DILOCO_LAZY_PIN=0) and the outer model in HBM
-(placement="device"), built in the order given; rounds x K back-to-back steps each, the
+and the outer model in HBM (placement="device"), built in the order given (round 4 also
+compared pageable host arenas and theta / wire / momentum carved from one allocation:
+profiles/r04_placement_ab_*.txt); rounds x K back-to-back steps each, the
 loop's GPU span / K (events on the step's stream) and the wall time / K. Under rocprofv3
 --kernel-trace the kernels' own durations tell GPU idle gaps from slower kernels.
 
-    python tools/placement_ab.py [rounds] [steps] [order: comma list of lazy,lazy_nopin,device]
+    python tools/placement_ab.py [rounds] [steps] [order: comma list of lazy,device]
 """
 import json
 import os
@@ -50,12 +51,10 @@ def main():
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     setups = {}
     for name in order:
-        os.environ["DILOCO_LAZY_PIN"] = "0" if name == "lazy_nopin" else "1"
-        os.environ["DILOCO_ONE_ARENA"] = "1" if name.endswith("_one") else "0"
         inner = torch.nn.Module()
         inner.ps = torch.nn.ParameterList([torch.nn.Parameter(t.view(s)) for t, s in zip(
             synth.outer_tree_device(spec, dev), shapes)])
-        outer = get_outer_model(inner, "device" if name.startswith("device") else None)
+        outer = get_outer_model(inner, "device" if name == "device" else None)
         opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9,
                                                    nesterov=True))
         synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, 0,
