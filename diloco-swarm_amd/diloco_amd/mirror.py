@@ -1178,8 +1178,7 @@ class DeviceOuterMirror:
         bufs: List[Optional[torch.Tensor]] = [None] * len(self.params)
         if momentum != 0:
             if self.d_mom is None:
-                self.d_mom = (self._mom_arena if self._mom_arena is not None
-                              else torch.zeros_like(self.d_theta))
+                self.d_mom = torch.zeros_like(self.d_theta)
                 plain = self._make_views(self.d_mom)
                 self._views["mom_plain"] = plain
                 self._views["mom"] = [self._momentum_buffer(v) for v in plain]
