@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
-"""Summarise bench.py lines from a scaling run (one JSON line per N: the driver's
-SCALE_rNN.json, or several bench outputs) against the N > 1 model of DESIGN.md §4: headline
-(RCCL sharded step), the replicated all-reduce variant, 64 MiB buckets, the ordered a2a step,
-the direct peer-access exchange, RCCL's own all_reduce busBW, the per-step grad sync (all_reduce
-and a2a), the RCCL setting variants and the link probe, per N.
+"""Summarise bench.py's compact lines from a scaling run (one JSON line per N: the driver's
+SCALE_rNN.json, or several bench outputs) against the N > 1 model of DESIGN.md §4: the headline
+(the reference's calls on the sharded exchange), its exchange roofline, the exchange efficiency
+per tree (the step's bus rate over RCCL's own all_reduce of the same bytes), every leg's GB/s and
+HBM bytes per parameter, and the parity self-checks, per N.
 
-    python tools/scale_report.py SCALE_r01.json [more files ...]
+    python tools/scale_report.py SCALE_r04.json [more files ...]
 """
 import json
 import sys
@@ -55,37 +55,27 @@ def model_gbs(n, link=76.8):
 
 def main():
     rows = sorted(lines(sys.argv[1:]), key=lambda d: d.get("n_gpus", 0))
-    hdr = ("N", "headline", "ms/step", "allreduce var", "64MiB", "a2a", "xgmi", "xgmi parity",
-           "rccl AR busBW", "frac of AR", "grad sync", "grad sync a2a", "link 1-peer",
-           "model@76.8")
-    print(" | ".join(hdr))
+    base = None
+    print(" | ".join(("N", "headline GB/s", "aggregate", "ms/step", "eff vs N=1", "xchg frac",
+                      "eff t125", "eff t1.3b", "model@76.8")))
     for d in rows:
         n = d.get("n_gpus") or 1
-        e = d.get("extra") or {}
-        p = d.get("parity") or {}
-        row = (n, d.get("value"), d.get("ms_per_step"),
-               val(e, "t125_allreduce_variant", "value"), val(e, "t125_bucket64MiB", "value"),
-               val(e, "t125_a2a", "value"),
-               val(e, "t125_xgmi_exchange", "value"), val(p, "xgmi", "ok"),
-               val(e, "rccl_allreduce_ref", "all_reduce", "busbw_GBs"),
-               val(d, "exchange_efficiency", "frac_of_rccl_allreduce"),
-               val(e, "t125_dp_grad_sync", "value"), val(e, "t125_dp_grad_sync_a2a", "value"),
-               val(e, "xgmi_link_probe", "one_peer_read_GBs"), model_gbs(n))
-        print(" | ".join("-" if x is None else (f"{x:.1f}" if isinstance(x, float) else str(x))
+        if n == 1:
+            base = d.get("value")
+        ee = d.get("exchange_efficiency") or {}
+        agg = d.get("value_aggregate")
+        eff = agg / (n * base) if agg and base else None
+        row = (n, d.get("value"), agg, d.get("ms_per_step"), eff,
+               val(d, "roofline", "frac") if n > 1 else None,
+               val(ee, "t125", "frac_of_rccl_allreduce"),
+               val(ee, "t1.3b", "frac_of_rccl_allreduce"), model_gbs(n))
+        print(" | ".join("-" if x is None else (f"{x:.3f}" if isinstance(x, float) else str(x))
                          for x in row))
-        for k in sorted(e):
-            if k.startswith("rccl_env_"):
-                print(f"    {k}: step {val(e, k, 'sharded_step', 'value')} GB/s, AR busBW "
-                      f"{val(e, k, 'rccl_allreduce_ref', 'all_reduce', 'busbw_GBs')}")
-        for k in sorted(d):
-            if k.startswith("exchange_efficiency_"):
-                print(f"    {k}: {d[k]}")
-        for k in ("t1.3b", "t1.3b_bf16_wire", "t1.3b_bf16_a2a", "t1.3b_int8_wire"):
-            if val(e, k, "value") is not None:
-                print(f"    {k}: {val(e, k, 'value')} GB/s, {val(e, k, 'ms_per_step')} ms/step")
-        for k in ("a2a", "a2a_bf16", "sharded", "bf16"):
-            if isinstance(p.get(k), dict):
-                print(f"    parity {k}: ok={p[k].get('ok')} identical={p[k].get('replicas_identical')}")
+        for k, v in sorted((d.get("legs") or {}).items()):
+            print(f"    {k}: {v.get('GBs')} GB/s, {v.get('ms')} ms, frac {v.get('frac')}, "
+                  f"{v.get('Bpp')} B/param")
+        bad = [k for k, v in (d.get("parity") or {}).items() if not v.get("ok")]
+        print(f"    parity: {'all ok' if not bad else 'FAILED ' + ', '.join(bad)}")
         if d.get("skipped_legs") or d.get("incomplete"):
             print(f"    skipped {d.get('skipped_legs')} incomplete {d.get('incomplete')}")
 
