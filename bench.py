@@ -54,7 +54,11 @@ LINE_MAX_BYTES = 4096       # the driver parses one stdout line; everything else
 
 
 def log(msg):
-    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+    """One stderr line per call, written whole (ranks share the stream), rank-tagged at N > 1."""
+    ws = os.environ.get("WORLD_SIZE", "1")
+    tag = f"[bench r{os.environ.get('RANK', '0')}/{ws}]" if ws != "1" else "[bench]"
+    sys.stderr.write(f"{tag} {msg}\n")
+    sys.stderr.flush()
 
 
 def load_pmc(tree):
@@ -960,6 +964,11 @@ def peer_access_legs(spec13, dev, ws, rank, steps, cap, parity_too, dump):
     dump(res)
     r = _guard(run_engine, spec13, dev, ws, rank, max(3, steps // 4), 1, torch.float32, cap,
                False, None, "xgmi_inner")
+    roof = r.get("roofline") if isinstance(r, dict) else None
+    if isinstance(roof, dict) and torch.cuda.device_count() < ws:
+        # a rehearsal with every rank on one GPU: the "peer" reads are local HBM reads
+        roof["frac_vs_link"], roof["frac"] = roof.get("frac"), None
+        roof["note"] = "ranks share one GPU: peer reads are local, the link peak does not apply"
     res["legs"][f"{spec13.name}_xgmi_inner"] = r
     dump(res)
     return res
