@@ -314,6 +314,64 @@ def _worker(rank, world, port, mode, num_stages, out):
                 comm.send_backward(src, (t * 2).detach(), meta)
             rec["seen"] = np.array(sorted(seen), dtype=np.float64).reshape(-1, 4)
         dist.barrier()
+    elif mode in ("adamw_lazy", "adamw_device"):
+        # an AdamW outer optimizer (src/utils.py:60-61) on the sharded exchange: AdamW reads
+        # .grad (a collective gather of the reduce-scattered slices, every rank in the same
+        # order) and writes θ in place; against the reference's calls on a plain deepcopy
+        # outer model with per-tensor all_reduce / n (src/comm.py:117-123), in this process
+        import copy
+
+        os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"
+        n = len(world_.dp_ranks)
+        if n > 2:  # AdamW's g / sqrt(v) amplifies any change of sum order: the rank-order form
+            import diloco_amd.comm as comm_mod
+
+            comm_mod.DP_EXCHANGE = "a2a"
+        inner = _micro_module(theta0, shapes)
+        ref_inner = copy.deepcopy(inner)
+        ref_outer = copy.deepcopy(ref_inner)
+        outer = get_outer_model(inner, placement="device" if mode == "adamw_device" else None)
+        cfg = _Cfg(type="AdamW", lr=0.01, weight_decay=0.1, betas=(0.9, 0.95))
+        opt, ref_opt = get_optimizer(outer, cfg), get_optimizer(ref_outer, cfg)
+        comm = TrainingComm(world_, (1, 1, 32), None)
+
+        def host(ts):
+            return np.concatenate([t.detach().numpy().reshape(-1) for t in ts])
+
+        for s in range(1, 4):
+            vals = synth.inner_tree([p.detach().numpy().reshape(-1).copy()
+                                     for p in ref_outer.parameters()], s, dp_rank)
+            with torch.no_grad():
+                for p, q, v in zip(inner.parameters(), ref_inner.parameters(), vals):
+                    p.copy_(torch.from_numpy(v).view(p.shape))
+                    q.copy_(p)
+            compute_pseudo_gradient(inner, outer)
+            comm.sync_gradients(outer)
+            opt.step()
+            sync_inner_model(outer, inner)
+            for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):
+                po.grad = po.data - pi.data
+                if n <= 2:
+                    dist.all_reduce(po.grad, op=dist.ReduceOp.SUM)
+                else:  # Σ in rank order, fp32, left to right
+                    parts = [torch.empty_like(po.grad) for _ in range(n)]
+                    dist.all_gather(parts, po.grad)
+                    po.grad = parts[0].clone()
+                    for q in parts[1:]:
+                        po.grad += q
+                po.grad /= n
+            ref_opt.step()
+            with torch.no_grad():
+                for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):
+                    pi.copy_(po)
+            rec[f"theta_s{s}"] = host(outer.parameters())
+            rec[f"inner_s{s}"] = host(inner.parameters())
+            rec[f"avg_s{s}"] = host(p.grad for p in outer.parameters())
+            rec[f"exp_avg_sq_s{s}"] = host(opt.state[p]["exp_avg_sq"] for p in outer.parameters())
+            rec[f"ref_theta_s{s}"] = host(ref_outer.parameters())
+            rec[f"ref_avg_s{s}"] = host(p.grad for p in ref_outer.parameters())
+            rec[f"ref_exp_avg_sq_s{s}"] = host(ref_opt.state[p]["exp_avg_sq"]
+                                               for p in ref_outer.parameters())
     elif mode == "outputs":
         comm = TrainingComm(world_, (1, 1, 4), None)
         o = Outputs(step=3, tokens=100 * (rank + 1), num_micro_batches=rank, time=1.0 + rank,
@@ -554,3 +612,22 @@ def test_dropin_int8_wire_matches_codec_restatement(mode, world):
             for k in ("theta", "buf", "avg"):
                 assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (mode, k, s)
             assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), (mode, s)
+
+
+@pytest.mark.parametrize("mode", ["adamw_lazy", "adamw_device"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_dropin_adamw_outer_optimizer_on_the_sharded_exchange(mode, world):
+    """An AdamW outer optimizer (the reference's get_optimizer allows it, src/utils.py:60-61)
+    on the default lazy host and the device outer model, several buckets: three outer steps
+    against the reference's calls on a plain deepcopy outer model in the same process, byte for
+    byte -- at 2 peers the default sharded exchange against per-tensor all_reduce / n; at 3
+    the rank-order exchange (DILOCO_DP_EXCHANGE=a2a) against a rank-order fp32 sum / n, since
+    AdamW's g / sqrt(v) turns any change of summation order into O(lr) differences where g
+    nearly cancels. θ equal across ranks and to the inner params."""
+    recs = _run(mode, world)
+    for rec in recs:
+        for s in (1, 2, 3):
+            assert rec[f"inner_s{s}"].tobytes() == rec[f"theta_s{s}"].tobytes(), (mode, s)
+            assert rec[f"theta_s{s}"].tobytes() == recs[0][f"theta_s{s}"].tobytes(), (mode, s)
+            for k in ("theta", "avg", "exp_avg_sq"):
+                assert rec[f"{k}_s{s}"].tobytes() == rec[f"ref_{k}_s{s}"].tobytes(), (mode, k, s)

@@ -343,6 +343,8 @@ def _worker(rank, world, port, mode, out):
                    if not normwise_ok(p.grad.cpu().numpy(), r.cpu().numpy(), 1e-6)]
         rec["bad"] = np.array(bad or [-1])
         rec["n"] = np.int64(len(ref))
+    elif mode in ("adamw_lazy", "adamw_device"):
+        rec = _adamw_outer_steps(rank, world, mode == "adamw_device")
     elif mode == "dropin_device_t13b_bf16_n8":
         rec = _bf16_dropin_codec_check(rank, world)
     elif mode in ("dropin_device_t125", "dropin_device_t125_bf16", "dropin_device_t13b",
@@ -353,6 +355,64 @@ def _worker(rank, world, port, mode, out):
     np.savez(os.path.join(out, f"{mode}_r{rank}.npz"), **rec)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _adamw_outer_steps(rank, world, device, steps=3):
+    """An AdamW outer optimizer (src/utils.py:60-61) through the four calls with the HIP
+    kernels, the sharded exchange in several buckets; beside it, in this process, the
+    reference's calls on a plain deepcopy CPU outer model with per-tensor all_reduce / n."""
+    import copy
+
+    from diloco_amd import synth
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+
+    os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
+    inner = _module(theta0, shapes, "cpu")
+    ref_outer = copy.deepcopy(inner)
+    outer = get_outer_model(inner, "device" if device else None)
+    inner = inner.to("cuda:0")
+    ref_inner = copy.deepcopy(inner)
+    cfg = _Cfg(type="AdamW", lr=0.01, weight_decay=0.1, betas=(0.9, 0.95))
+    opt, ref_opt = get_optimizer(outer, cfg), get_optimizer(ref_outer, cfg)
+    assert type(opt) is torch.optim.AdamW
+    comm = TrainingComm(World.from_default_group(1), (1, 1, 32), None)
+    rec = {}
+    for s in range(1, steps + 1):
+        vals = synth.inner_tree([p.detach().numpy().reshape(-1).copy()
+                                 for p in ref_outer.parameters()], s, rank)
+        with torch.no_grad():
+            for p, q, v in zip(inner.parameters(), ref_inner.parameters(), vals):
+                p.copy_(torch.from_numpy(v).view(p.shape))
+                q.copy_(p)
+        compute_pseudo_gradient(inner, outer)
+        comm.sync_gradients(outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):  # src/utils.py:221
+            po.grad = po.data - pi.data.to("cpu")
+            dist.all_reduce(po.grad, op=dist.ReduceOp.SUM)  # src/comm.py:122-123
+            po.grad /= world
+        ref_opt.step()
+        with torch.no_grad():
+            for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):
+                pi.copy_(po)
+        torch.cuda.synchronize()
+        rec[f"theta_s{s}"] = _flat(outer.parameters())
+        rec[f"inner_s{s}"] = _flat(inner.parameters())
+        rec[f"avg_s{s}"] = _flat(p.grad for p in outer.parameters())
+        rec[f"exp_avg_sq_s{s}"] = _flat(opt.state[p]["exp_avg_sq"] for p in outer.parameters())
+        rec[f"ref_theta_s{s}"] = _flat(ref_outer.parameters())
+        rec[f"ref_avg_s{s}"] = _flat(p.grad for p in ref_outer.parameters())
+        rec[f"ref_exp_avg_sq_s{s}"] = _flat(ref_opt.state[p]["exp_avg_sq"]
+                                            for p in ref_outer.parameters())
+    return rec
 
 
 def _bf16_dropin_codec_check(rank, world, steps=2, tree="t1.3b"):
@@ -905,3 +965,17 @@ def test_dropin_int8_wire_two_peers_on_gpu(mode):
             for k in ("theta", "buf", "avg"):
                 assert rec[f"{k}_s{s}"].tobytes() == exp[f"{k}_s{s}"].tobytes(), (mode, k, s)
             assert rec[f"inner_s{s}"].tobytes() == exp[f"theta_s{s}"].tobytes(), (mode, s)
+
+
+@pytest.mark.parametrize("mode", ["adamw_lazy", "adamw_device"])
+def test_dropin_adamw_outer_optimizer_two_peers_on_gpu(mode):
+    """An AdamW outer optimizer (src/utils.py:60-61) on the default lazy host and the device
+    outer model with the HIP kernels: two processes, the sharded exchange in several buckets,
+    AdamW reading the gathered .grad and writing θ in place; three outer steps byte-equal to
+    the reference's calls on a plain deepcopy outer model (per-tensor all_reduce / n)."""
+    recs = _run(mode)
+    for rec in recs:
+        for s in (1, 2, 3):
+            assert rec[f"inner_s{s}"].tobytes() == rec[f"theta_s{s}"].tobytes(), (mode, s)
+            for k in ("theta", "avg", "exp_avg_sq"):
+                assert rec[f"{k}_s{s}"].tobytes() == rec[f"ref_{k}_s{s}"].tobytes(), (mode, k, s)

@@ -538,3 +538,45 @@ def test_checkpoint_resume_through_state_dicts(placement):
                  for p in outer2.parameters()).tobytes() == g["buf_s2"].tobytes()
     assert _host(p.grad for p in outer2.parameters()).tobytes() == g["delta_s2_r0"].tobytes()
     assert _host(inner2.parameters()).tobytes() == g["theta_s2"].tobytes()
+
+
+ADAMW_CFG = _Cfg(type="AdamW", lr=0.01, weight_decay=0.1, betas=(0.9, 0.95))
+
+
+@pytest.mark.parametrize("placement", [None, "device"])
+def test_adamw_outer_optimizer_matches_plain_torch(placement):
+    """The reference's get_optimizer also builds AdamW for the outer optimizer
+    (src/utils.py:60-61, src/train.py:420-421). Stock torch AdamW on the default lazy host and
+    on the device outer model: it reads .grad (the pending delta completed first) and updates
+    θ with in-place ops the mirror must see before sync_inner_model. Three outer steps equal,
+    byte for byte, the same calls on a plain deepcopy outer model (src/utils.py:213-226)."""
+    import copy
+
+    inner, outer = _models(None) if placement is None else _device_models(True)
+    ref_inner = copy.deepcopy(inner)
+    ref_outer = copy.deepcopy(ref_inner).to("cpu")  # src/utils.py:215-216
+    opt = get_optimizer(outer, ADAMW_CFG)
+    ref_opt = torch.optim.AdamW(ref_outer.parameters(), lr=0.01, weight_decay=0.1,
+                                betas=(0.9, 0.95))
+    assert type(opt) is torch.optim.AdamW
+    for s in (1, 2, 3):
+        _set_inner(inner, outer, s)
+        with torch.no_grad():
+            for p, q in zip(ref_inner.parameters(), inner.parameters()):
+                p.copy_(q)
+        compute_pseudo_gradient(inner, outer)
+        for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):  # :218-221
+            po.grad = po.data - pi.data.to(po.device)
+        opt.step()
+        ref_opt.step()
+        sync_inner_model(outer, inner)
+        for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):  # :223-226
+            pi.data.copy_(po.data)
+        want = _host(ref_outer.parameters()).tobytes()
+        assert _host(p.detach().cpu() for p in outer.parameters()).tobytes() == want, s
+        assert _host(inner.parameters()).tobytes() == want, s
+        assert _host(p.grad.cpu() for p in outer.parameters()).tobytes() == \
+            _host(p.grad for p in ref_outer.parameters()).tobytes(), s
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert _host(opt.state[p][k].cpu() for p in outer.parameters()).tobytes() == \
+                _host(ref_opt.state[p][k] for p in ref_outer.parameters()).tobytes(), (s, k)
