@@ -580,3 +580,52 @@ def test_adamw_outer_optimizer_matches_plain_torch(placement):
         for k in ("exp_avg", "exp_avg_sq"):
             assert _host(opt.state[p][k].cpu() for p in outer.parameters()).tobytes() == \
                 _host(ref_opt.state[p][k] for p in ref_outer.parameters()).tobytes(), (s, k)
+
+
+@pytest.mark.parametrize("momentum,nesterov", [(0.0, False), (0.9, False), (0.5, True)])
+@pytest.mark.parametrize("placement", [None, "device"])
+def test_outer_sgd_other_configs_match_plain_torch(placement, momentum, nesterov):
+    """OuterSGD (get_optimizer's SGD on the outer model, src/utils.py:62-63) for the other
+    configurations an OptimizerConfig can hold -- no momentum, heavy-ball momentum, another
+    Nesterov coefficient -- three outer steps byte-equal to torch.optim.SGD on a plain deepcopy
+    outer model, quiet (the fused pass) and with .grad read between the calls."""
+    import copy
+
+    for quiet in (True, False):
+        inner, outer = _models(None) if placement is None else _device_models(True)
+        ref_inner = copy.deepcopy(inner)
+        ref_outer = copy.deepcopy(ref_inner)
+        cfg = _Cfg(type="SGD", lr=0.7, momentum=momentum, nesterov=nesterov)
+        opt, ref_opt = get_optimizer(outer, cfg), get_optimizer(ref_outer, cfg)
+        assert type(opt).__name__ == "OuterSGD" and type(ref_opt) is torch.optim.SGD
+        for s in (1, 2, 3):
+            _set_inner(inner, outer, s)
+            with torch.no_grad():
+                for p, q in zip(ref_inner.parameters(), inner.parameters()):
+                    p.copy_(q)
+            compute_pseudo_gradient(inner, outer)
+            if not quiet:
+                mid = _host(p.grad.cpu() for p in outer.parameters())
+            opt.step()
+            sync_inner_model(outer, inner)
+            for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):
+                po.grad = po.data - pi.data
+            ref_opt.step()
+            for po, pi in zip(ref_outer.parameters(), ref_inner.parameters()):
+                pi.data.copy_(po.data)
+            want = _host(ref_outer.parameters()).tobytes()
+            where = (placement, momentum, nesterov, quiet, s)
+            assert _host(p.detach().cpu() for p in outer.parameters()).tobytes() == want, where
+            assert _host(inner.parameters()).tobytes() == want, where
+            g = _host(p.grad for p in ref_outer.parameters()).tobytes()
+            assert _host(p.grad.cpu() for p in outer.parameters()).tobytes() == g, where
+            if not quiet:
+                assert mid.tobytes() == g, where
+            if momentum:
+                assert _host(opt.state[p]["momentum_buffer"].cpu()
+                             for p in outer.parameters()).tobytes() == _host(
+                    ref_opt.state[p]["momentum_buffer"] for p in ref_outer.parameters()
+                ).tobytes(), where
+            else:
+                assert all(opt.state[p].get("momentum_buffer") is None
+                           for p in outer.parameters()), where
