@@ -37,6 +37,8 @@ import threading
 import time
 from datetime import timedelta
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "diloco-swarm_amd"))
 
@@ -213,8 +215,10 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
     model stepped on its HBM twin; "device": the outer model in HBM): K steps back to back
     between barrier + synchronize (the four Python calls of step k+1 are issued while step k's
     kernels run). synced: a device synchronize after every step, as the reference's loop has
-    around its outer step (src/train.py:244), so the calls' host time is exposed. cold (N = 1):
-    then K more steps, each after an Infinity-Cache scrub outside the events."""
+    around its outer step (src/train.py:244), so the calls' host time is exposed; each step is
+    timed on its own and the value is the median step's (one host stall on a shared box moved a
+    10-step mean from 0.68 to 5.3 ms; the mean stays in the record). cold (N = 1): then K more
+    steps, each after an Infinity-Cache scrub outside the events."""
     from diloco_amd.utils import compute_pseudo_gradient, sync_inner_model
 
     inner, outer, opt, comm = _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange,
@@ -234,12 +238,18 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
     ev[0].record()
+    per = []
     for _ in range(steps):
+        t1 = time.perf_counter()
         one()
+        per.append(time.perf_counter() - t1)
     ev[1].record()
     _sync(ws)
     dt = _max_over_ranks((time.perf_counter() - t0) / steps, dev, ws)
     loop_ms = ev[0].elapsed_time(ev[1]) / steps
+    mean_ms = dt * 1e3
+    if synced:  # every step ended with a synchronize: its own wall time is the step's
+        dt = _max_over_ranks(float(np.median(per)), dev, ws)
     P = spec.total()
     mm = outer._diloco_mirror
     m = getattr(mm, "dev", mm)  # the lazy host placement steps on its HBM twin
@@ -251,6 +261,8 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
            "value_aggregate": ws * 4.0 * P / dt / 1e9, "loop_gpu_ms_per_step": round(loop_ms, 5),
            "wire": wire, "exchange": ex if ws > 1 else "none (one peer)",
            "hbm_bytes_per_param": round(bpp, 3), "synced": synced,
+           **({"mean_ms_per_step": round(mean_ms, 5), "timing": "median step (synced)"}
+              if synced else {}),
            "placement": ("device" if mm is m else "host (write_back lazy: HBM twin)")}
     if ws == 1:
         # one kernel per step: its average launch duration is the timed loop's GPU span / K
@@ -883,8 +895,6 @@ def xgmi_link_probe(dev, ws, rank, reps=5, mib=256):
     link each), then from every peer at once, then from its own HBM; max time over ranks."""
     import ctypes
 
-    import numpy as np
-
     from diloco_amd.xgmi import PeerMap
 
     n = (mib << 20) // 4
@@ -1387,7 +1397,7 @@ def main():
                 leg(f"{es.name}_int8", run_q8, es, dev, ws, rank, ks, 1, cap)
             leg(f"{spec.name}_dropin_device", run_dropin, spec, dev, ws, rank, a.steps,
                 a.warmup, "f32", None, "sharded", False, False, "device")
-            leg(f"{spec.name}_dropin_synced", run_dropin, spec, dev, ws, rank, 10, 1, "f32",
+            leg(f"{spec.name}_dropin_synced", run_dropin, spec, dev, ws, rank, 30, 1, "f32",
                 None, "sharded", False, True)
             leg("dropin_pcie", dropin_pcie, spec, dev, ws, rank, 5)
         else:
