@@ -201,8 +201,9 @@ def _free_port():
 
 def _spawn(dev, cases):
     out = tempfile.mkdtemp(prefix="dl_fuzz_")
-    mp.spawn(_worker, args=(WORLD, _free_port(), out, dev, list(cases)), nprocs=WORLD,
-             join=True)
+    # CPU: forked workers (no HIP state in this process to inherit); the GPU: fresh ones
+    mp.start_processes(_worker, args=(WORLD, _free_port(), out, dev, list(cases)), nprocs=WORLD,
+                       join=True, start_method="fork" if dev == "cpu" else "spawn")
     bad = []
     for r in range(WORLD):
         with open(os.path.join(out, f"r{r}.txt")) as f:
