@@ -53,7 +53,7 @@ def _perturb(params, step):
 
 
 def _win(t, lo, hi):
-    return t.reshape(-1)[lo:hi].cpu().numpy().copy()
+    return t.detach().reshape(-1)[lo:hi].cpu().numpy().copy()
 
 
 def _q8_step(st, inner):
@@ -142,4 +142,63 @@ def test_gradsync_round_trip_beyond_2_31():
             assert _win(gs.wire, o + lo, o + hi).tobytes() == want[i][k].tobytes(), (i, lo)
     gs.close()
     del gs, params
+    torch.cuda.empty_cache()
+
+
+class _Cfg:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+@pytest.mark.parametrize("placement", ["device", None])
+def test_dropin_calls_beyond_2_31(placement):
+    """The reference's four calls (src/train.py:263-269) over the same tree: get_outer_model on
+    the device placement and on the default lazy host one (pinned host arenas of 8.6 GB each,
+    one DMA per read), get_optimizer's OuterSGD, one peer. Two outer steps; θ, .grad, the
+    momentum (opt.state) and the inner params bit-exact against the C oracle on the windows."""
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+    import tempfile
+    import torch.distributed as dist
+
+    free, _total = torch.cuda.mem_get_info()
+    if free < 80 << 30:
+        pytest.skip(f"needs ~50 GB of free HBM, {free >> 30} GiB free")
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", init_method="file://" + tempfile.mktemp(prefix="dl_pg_"),
+                                rank=0, world_size=1)
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList([torch.nn.Parameter(p) for p in _params()])
+    outer = get_outer_model(inner, placement)
+    opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
+    comm = TrainingComm(World.from_default_group(1), (1, 1, 8), None)
+    params = list(inner.parameters())
+    wins = [_windows(p.numel()) for p in params]
+    states = [[oracle.OuterState([_win(p, lo, hi)]) for lo, hi in ws]
+              for p, ws in zip(params, wins)]
+    for step in (1, 2):
+        with torch.no_grad():
+            _perturb(params, step)
+        inner_w = [[_win(p, lo, hi) for lo, hi in ws] for p, ws in zip(params, wins)]
+        compute_pseudo_gradient(inner, outer)
+        comm.sync_gradients(outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        ops = list(outer.parameters())
+        for i, ws in enumerate(wins):
+            for k, (lo, hi) in enumerate(ws):
+                st = states[i][k]
+                deltas, avg = st.step([[inner_w[i][k]]])
+                where = f"{placement} step {step} tensor {i} [{lo}, {hi})"
+                got = _win(ops[i].detach(), lo, hi)
+                assert got.tobytes() == st.theta[0].tobytes(), where
+                assert _win(params[i].detach(), lo, hi).tobytes() == got.tobytes(), where
+                assert _win(ops[i].grad, lo, hi).tobytes() == avg[0].tobytes(), where + " grad"
+                buf = opt.state[ops[i]]["momentum_buffer"]
+                assert _win(buf, lo, hi).tobytes() == st.buf[0].tobytes(), where + " mom"
+    outer._diloco_mirror.close()
+    del outer, opt, inner, params
     torch.cuda.empty_cache()
