@@ -42,6 +42,7 @@ from . import _lib
 from .kernels import default_kernels
 from .outer import pipelined_buckets
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_GRAD, SLOT_INNER
+from .staging import before_collective, collective
 
 ALL = _lib.ALL_BUCKETS
 S_CHUNK = _lib.CHUNK_ELEMS  # elements per tree chunk (one int8 slot each)
@@ -79,8 +80,10 @@ def ordered_average(k, tree, wire: torch.Tensor, recv: torch.Tensor, group, n: i
     landing buffer the wire's size."""
     for lo, hi in tree.bucket_ranges:
         s = (hi - lo) // n
+        before_collective(group, wire)
         dist.all_to_all_single(recv[lo:hi], wire[lo:hi], group=group)
         k.shard_reduce_avg(recv[lo:hi], n, wire[lo + rank * s:lo + (rank + 1) * s])
+        before_collective(group, wire)
         dist.all_gather_into_tensor(wire[lo:hi], wire[lo + rank * s:lo + (rank + 1) * s],
                                     group=group)
 
@@ -290,7 +293,8 @@ class HostOuterMirror:
 
         pipelined_buckets(
             self.tree.n_buckets, lambda b: None,
-            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
+            lambda b: collective(dist.all_reduce, group, view(b), op=dist.ReduceOp.SUM,
+                                  group=group, async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
         )
         self._grads_to_host()
@@ -787,6 +791,7 @@ class DeviceOuterMirror:
             a, e = self._own(b, n, r)
             if mode == "a2a":
                 self.k.shard_reduce_avg(self.d_recv[lo:hi], n, self.d_wire[a:e])
+            before_collective(g, self.d_wire)
             dist.all_gather_into_tensor(self.d_wire[lo:hi], self.d_wire[a:e], group=g)
 
     def gather_momentum(self) -> None:
@@ -799,6 +804,7 @@ class DeviceOuterMirror:
         for b in range(self.tree.n_buckets):
             lo, hi = self.tree.bucket_ranges[b]
             a, e = self._own(b, n, r)
+            before_collective(g, self.d_mom)
             dist.all_gather_into_tensor(self.d_mom[lo:hi], self.d_mom[a:e], group=g)
 
     def _sharded_sgd(self, mom, lr, momentum, nesterov, first, target) -> None:
@@ -822,6 +828,7 @@ class DeviceOuterMirror:
                 self.k.shard_reduce_avg(self.d_recv[lo:hi], n, self.d_wire[a:e])
             self.k.shard_sgd(self.d_wire[a:e], 1 if mode == "a2a" else n, self.d_theta[a:e],
                              None if mom is None else mom[a:e], lr, momentum, nesterov, first)
+            before_collective(g, self.d_theta)
             ags[b] = dist.all_gather_into_tensor(self.d_theta[lo:hi], self.d_theta[a:e],
                                                  group=g, async_op=True)
             if b >= 1:
@@ -952,7 +959,8 @@ class DeviceOuterMirror:
             return
         pipelined_buckets(
             self.tree.n_buckets, pack or (lambda b: None),
-            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
+            lambda b: collective(dist.all_reduce, group, view(b), op=dist.ReduceOp.SUM,
+                                  group=group, async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
         )
 
@@ -989,7 +997,8 @@ class DeviceOuterMirror:
             return
         pipelined_buckets(
             self.tree.n_buckets, pack,
-            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group, async_op=True),
+            lambda b: collective(dist.all_reduce, group, view(b), op=dist.ReduceOp.SUM,
+                                  group=group, async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, w16, num_peers, -1, self.d_wire),
         )
 
@@ -1023,6 +1032,7 @@ class DeviceOuterMirror:
                 pack(b)
             lo, hi = self.tree.bucket_ranges[b]
             a, e = self._own(b, n, rank)
+            before_collective(group, self.d_wire)
             if mode == "a2a":
                 works.append(dist.all_to_all_single(self.d_recv[lo:hi], self.d_wire[lo:hi],
                                                     group=group, async_op=True))
@@ -1097,6 +1107,7 @@ class DeviceOuterMirror:
 
         def a2a(b):
             nch, m, _, _ = q["plan"][b]
+            before_collective(group, q["recv"][b % 2])
             return dist.all_to_all_single(q["recv"][b % 2][:n * m * S], self._q8_region(q, b),
                                           group=group, async_op=True)
 
@@ -1111,6 +1122,7 @@ class DeviceOuterMirror:
             nch, m, _, rb = q["plan"][b]
             red = q["red"][rb * S:(rb + m) * S]
             self.k.q8_reduce(q["recv"][b % 2][:n * m * S], n, m, n, red)
+            before_collective(group, red)
             works[b] = dist.all_gather_into_tensor(self._q8_region(q, b), red, group=group,
                                                    async_op=True)
         self._works = works
@@ -1161,6 +1173,7 @@ class DeviceOuterMirror:
         for b in range(self.tree.n_buckets):
             if pack is not None:
                 pack(b)
+            before_collective(group, view(b))
             works.append(dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group,
                                          async_op=True))
         self._works = works

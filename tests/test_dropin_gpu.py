@@ -480,7 +480,18 @@ def _bf16_dropin_codec_check(rank, world, steps=2, tree="t1.3b"):
             g = window(ops[t].grad, t, lo, m)
             err = np.abs(g.astype(np.float64) - g32)
             if not np.all(err <= bound):
-                bad.append(f"step {s} tensor {t} codec bound")
+                i = int(np.argmax(err / np.maximum(bound, 1e-38)))
+                over = np.flatnonzero(err > bound)
+                # per bad element: the rank whose delta, left out, explains the sum
+                gn = g.astype(np.float64) * world
+                dd = np.stack(d).astype(np.float64)[:, over]
+                miss = np.argmin(np.abs((dd.sum(0) - gn[over])[None, :] - dd), axis=0)
+                runs = np.split(over, np.flatnonzero(np.diff(over) != 1) + 1)
+                bad.append(f"step {s} tensor {t} codec bound: {over.size} of {m} elements, "
+                           f"missing ranks {sorted(set(miss.tolist()))}, runs "
+                           f"{[(int(lo + r[0]), int(r.size)) for r in runs[:6]]}"
+                           f"{'...' if len(runs) > 6 else ''} ({len(runs)} runs); element "
+                           f"{lo + i} g {g[i]!r} fp32 avg {g32[i]!r} bound {bound[i]!r}")
             worst = max(worst, float((err / np.maximum(bound, 1e-38)).max()))
             th_exp, buf_exp = th0.copy(), (np.empty_like(th0) if buf0 is None else buf0.copy())
             oracle.sgd(th_exp, buf_exp, g, 0.7, 0.9, True, s == 1)
