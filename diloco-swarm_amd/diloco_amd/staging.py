@@ -20,19 +20,22 @@ from typing import Dict, Optional
 import torch
 import torch.distributed as dist
 
-_GLOO: Dict[int, bool] = {}
+# keyed by the group object itself (held here, so a destroyed group's id cannot be reused by a
+# new group of another backend and inherit its answer); None = the default group, which
+# destroy_process_group + init_process_group can replace, so it is never cached
+_GLOO: Dict[dist.ProcessGroup, bool] = {}
 
 
 def host_staged(group: Optional[dist.ProcessGroup]) -> bool:
     """The group's collectives stage device tensors through host memory (gloo)."""
-    key = id(group)
-    v = _GLOO.get(key)
+    v = None if group is None else _GLOO.get(group)
     if v is None:
         try:
             v = dist.get_backend(group) == "gloo"
         except (RuntimeError, ValueError):
             v = False
-        _GLOO[key] = v
+        if group is not None:
+            _GLOO[group] = v
     return v
 
 
