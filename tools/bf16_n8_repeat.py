@@ -22,9 +22,23 @@ import torch.multiprocessing as mp  # noqa: E402
 
 
 def _patch(variant):
-    from diloco_amd import mirror
+    from diloco_amd import mirror, staging
 
-    if variant == "sync_pack":
+    if variant in ("nostage", "fence"):
+        # nostage: no wait before a gloo collective (the code before diloco_amd.staging);
+        # fence: no host wait either, but every XCD's L2 written back at system scope on the
+        # caller's stream (dl_sys_fence) ahead of the collective -- if the race is gloo's DMA
+        # copy reading HBM under dirty L2 lines, this alone removes it
+        from diloco_amd.kernels import default_kernels
+
+        k = default_kernels()
+
+        def before(group, t):
+            if variant == "fence" and t.is_cuda and staging.host_staged(group):
+                k.sys_fence(t.device)
+        staging.before_collective = before
+        mirror.before_collective = before
+    elif variant == "sync_pack":
         orig = mirror.DeviceOuterMirror._launch_reductions
 
         def launch(self, pack, view, group):
@@ -69,11 +83,15 @@ def _worker(rank, world, port, variant, out):
 if __name__ == "__main__":
     import test_dropin_gpu as t
 
+    import time
+
     k = int(sys.argv[1])
-    for variant in sys.argv[2:]:
-        for i in range(k):
+    for i in range(k):  # variants interleaved, so a drift of the box hits each alike
+        for variant in sys.argv[2:]:
+            t0 = time.time()
             out = tempfile.mkdtemp()
             mp.spawn(_worker, args=(8, t._free_port(), variant, out), nprocs=8, join=True)
             recs = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(8)]
             bad = [str(b)[:400] for r in recs[:1] for b in r["bad"] if str(b) != "none"]
-            print(variant, i, round(float(recs[0]["worst"]), 4), len(bad), bad[:1], flush=True)
+            print(variant, i, round(float(recs[0]["worst"]), 4), len(bad), bad[:1],
+                  f"{time.time() - t0:.0f}s", flush=True)
