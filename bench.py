@@ -81,7 +81,8 @@ def setup_dist(n_gpus):
     if ws != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={ws}; launch N>1 with torchrun")
     # DILOCO_BENCH_BACKEND=gloo rehearses the N > 1 code path with several ranks on one GPU
-    # (RCCL refuses two ranks per device); the driver's multi-GPU runs use RCCL.
+    # (RCCL refuses two ranks per device): the DP group is then gloo too. The driver's
+    # multi-GPU runs use RCCL for it.
     backend = os.environ.get("DILOCO_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local %= max(1, torch.cuda.device_count())
@@ -91,16 +92,40 @@ def setup_dist(n_gpus):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if ws > 1:
-        # a hung collective becomes an error after 5 minutes instead of the 10-minute default
-        kw = {"device_id": dev} if backend == "nccl" else {}
-        dist.init_process_group(backend, timeout=timedelta(minutes=5), **kw)
+        # the process groups src/train.py runs with: a gloo default group (src/world.py:32-33)
+        # and, for every device collective, the DP group TrainingComm's DPSync creates over it
+        # (an RCCL subgroup, use_local_synchronization=True; dp_group() below). A hung
+        # collective becomes an error after 5 minutes instead of the 10-minute default.
+        dist.init_process_group("gloo", timeout=timedelta(minutes=5))
     return ws, rank, dev
+
+
+_COMM: dict = {}
+
+
+def training_comm(n_embd=768):
+    """The run's one TrainingComm (src/train.py:291 makes one), over the default group."""
+    if "comm" not in _COMM:
+        from diloco_amd.comm import TrainingComm
+        from diloco_amd.world import World
+
+        _COMM["comm"] = TrainingComm(World.from_default_group(1), (1, 1, n_embd), None)
+    return _COMM["comm"]
+
+
+def dp_group(dev):
+    """The group of every device collective in the bench at N > 1: DPSync.dp_group, exactly
+    the group TrainingComm.sync_gradients reduces over in src/train.py's wiring. None at one
+    rank (no collective is made)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return None
+    return training_comm().dp.dp_group(dev)
 
 
 def _max_over_ranks(x, dev, ws):
     if ws == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64)  # host value, the gloo default group
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -164,8 +189,6 @@ def dropin_bpp(ws, exchange, wire="f32"):
     return 12 + 20.0 / ws + 8
 
 
-_COMM: dict = {}
-
 
 def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange, placement=None):
     """The objects src/train.py builds for the outer step (train.py:375-421): an inner model on
@@ -173,9 +196,7 @@ def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange, placement=Non
     HBM twin (write_back="lazy") -- get_optimizer(outer, nesterov cfg), TrainingComm."""
     from types import SimpleNamespace
 
-    from diloco_amd.comm import TrainingComm
     from diloco_amd.utils import get_optimizer, get_outer_model
-    from diloco_amd.world import World
 
     if not dist.is_initialized():
         import tempfile
@@ -198,10 +219,9 @@ def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange, placement=Non
             else:
                 os.environ[knob] = prev
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
-    if "comm" not in _COMM:  # one TrainingComm per run, as src/train.py:291 makes (its DP group
-        # -- an RCCL communicator at N > 1 -- is created once and shared by every leg)
-        _COMM["comm"] = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
-    comm = _COMM["comm"]
+    # one TrainingComm per run, as src/train.py:291 makes (its DP group -- an RCCL
+    # communicator at N > 1 -- is created once and shared by every leg)
+    comm = training_comm(spec.n_embd)
     # inner = θ_0 + this rank's noise (H inner steps' stand-in); later steps see inner = θ
     synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
                             out=[p.data.view(-1) for p in inner.parameters()])
@@ -366,7 +386,7 @@ def build(spec, dev, rank, wire, cap, fuse=True, shard=None, exchange="rccl", ke
     params = [t.view(s) for t, s in zip(theta0, shapes)]
     eng = OuterSync(params, lr=0.7, momentum=0.9, nesterov=True, wire_dtype=wire,
                     bucket_cap_elems=cap, fuse_single=fuse, shard=shard, exchange=exchange,
-                    keep_wire=keep_wire, group=group)
+                    keep_wire=keep_wire, group=group if group is not None else dp_group(dev))
     # inner = θ_0 + this rank's noise (stands in for H inner steps)
     synth.inner_tree_device([p.view(-1) for p in params], 1, rank, out=[p.view(-1) for p in params])
     return eng
@@ -523,7 +543,7 @@ def _identical(t, ws):
     bits = t.view(torch.int32).to(torch.int64).sum()
     ck = torch.stack([bits, -bits])
     if ws > 1:
-        dist.all_reduce(ck, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ck, op=dist.ReduceOp.MAX, group=dp_group(t.device))
     return bool(ck[0].item() == -ck[1].item())
 
 
@@ -740,7 +760,8 @@ def rccl_reference(dev, ws, rank, elems, reps=5):
     `elems` elements, and a reduce_scatter + all_gather pair of the same size, back to back,
     max over ranks. busBW = 2(n-1)/n · bytes / t (the nccl-tests convention)."""
     out = {}
-    if dist.get_backend() == "gloo":
+    group = dp_group(dev)
+    if dist.get_backend(group) == "gloo":
         # a gloo rehearsal on one GPU stages whole tensors through host memory in every rank:
         # 8 ranks x a 5 GB tree exceed the box's host-memory cap, and the rate is gloo's anyway
         cap = (256 << 20) // 4 // (64 * ws) * (64 * ws)
@@ -757,10 +778,10 @@ def rccl_reference(dev, ws, rank, elems, reps=5):
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
             if name == "all_reduce":
-                dist.all_reduce(x)
+                dist.all_reduce(x, group=group)
             else:
-                dist.reduce_scatter_tensor(sh, x)
-                dist.all_gather_into_tensor(x, sh)
+                dist.reduce_scatter_tensor(sh, x, group=group)
+                dist.all_gather_into_tensor(x, sh, group=group)
         e1.record()
         e1.synchronize()
         ms = _max_over_ranks(e0.elapsed_time(e1) / reps, dev, ws)
@@ -798,7 +819,7 @@ def gradsync_rate(spec, dev, ws, rank, steps, exchange="rccl"):
     for i, p in enumerate(params):
         p.grad = torch.empty_like(p)
         synth.fill_device(p.grad.view(-1), synth.noise_seed(9, rank), i, 0.0, 1e-3)
-    gs = GradSync(params, None, ws, exchange=exchange)
+    gs = GradSync(params, dp_group(dev), ws, exchange=exchange)
     gs.sync()
     _sync(ws)
     t0 = time.perf_counter()
@@ -817,7 +838,10 @@ def run_two_stages(spec, dev, ws, rank, steps, warmup, cap):
     """The reference's two-stage layout (src/world.py:96-97, stage = rank % 2): two disjoint DP
     groups of ws/2 ranks run the sharded outer step at the same time, each over its own RCCL
     communicator. value = 2 · 4P / t_step (two trees reduced per step)."""
-    groups = [dist.new_group([r for r in range(ws) if r % 2 == s]) for s in range(2)]
+    from diloco_amd import comm
+
+    groups = [dist.new_group([r for r in range(ws) if r % 2 == s], backend=comm.DP_BACKEND)
+              for s in range(2)]
     eng = build(spec, dev, rank, torch.float32, cap, group=groups[rank % 2])
     for _ in range(max(warmup, 1)):
         eng.step()
@@ -841,10 +865,8 @@ def dropin_pcie(spec, dev, ws, rank, steps):
     PCIe-inclusive rate DESIGN.md §7 records (not the headline)."""
     from types import SimpleNamespace
 
-    from diloco_amd.comm import TrainingComm
     from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
                                   sync_inner_model)
-    from diloco_amd.world import World
 
     shapes = [s for _, s in spec.params()]
     inner = torch.nn.Module()
@@ -852,7 +874,7 @@ def dropin_pcie(spec, dev, ws, rank, steps):
         [torch.nn.Parameter(t.view(s)) for t, s in zip(synth.outer_tree_device(spec, dev), shapes)])
     outer = get_outer_model(inner, "host", write_back="sync")  # host tensors authoritative
     opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
-    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    comm = training_comm(spec.n_embd)
     synth.inner_tree_device([p.data.view(-1) for p in inner.parameters()], 1, rank,
                             out=[p.data.view(-1) for p in inner.parameters()])
     phases = [0.0] * 4
@@ -1355,11 +1377,12 @@ def main():
     em.build = lambda: assemble_line(meta, head, cpu, legs, parity, exch or None)
     log(f"headline done at {em.elapsed():.1f} s: {head['value']:.1f} GB/s")
 
-    def leg(name, fn, *args, into=legs):
+    def leg(name, fn, *args, into=legs, always=False):
         """One side leg, in the same order on every rank; skipped (on every rank alike: the
-        decision uses the max over ranks of the elapsed time) past the soft budget."""
+        decision uses the max over ranks of the elapsed time) past the soft budget, unless
+        `always` (the parity checks the line must carry)."""
         t = _max_over_ranks(em.elapsed(), dev, ws)
-        if t > soft:
+        if t > soft and not always:
             em.skipped.append(name)
             log(f"skipping {name}: {t:.0f} s elapsed > soft budget {soft:.0f} s")
             return None
@@ -1384,6 +1407,15 @@ def main():
             cpu = isolated_legs(a, dev, ws, rank, 150.0, "cpu_baseline", HIDE_GPUS)
         em.detail["cpu_baseline"] = cpu
         log(f"cpu_baseline done at {em.elapsed():.1f} s")
+
+    # then the parity the line must carry at any N, ahead of every side leg (a slow side leg
+    # can no longer cost the line its parity): the f32 average against torch, and at N > 1
+    # the headline path's exchanges behind the reference's calls against each other
+    if not a.no_parity and not a.only_headline:
+        leg("f32", parity_f32, dev, ws, rank, into=parity, always=True)
+        if ws > 1:
+            leg("dropin_exchanges", parity_dropin_exchanges, dev, ws, rank, into=parity,
+                always=True)
 
     if not a.only_headline:
         if ws == 1:
@@ -1436,13 +1468,11 @@ def main():
                 leg(f"{spec.name}_two_stages", run_two_stages, spec, dev, ws, rank, a.steps,
                     a.warmup, cap)
         if not a.no_parity:
-            leg("f32", parity_f32, dev, ws, rank, into=parity)
             leg("bf16", codec_parity, get_tree("tiny"), dev, ws, rank, 1 << 20, into=parity)
             leg("int8", parity_q8, dev, ws, rank, into=parity)
             leg("sharded", parity_sharded, dev, ws, rank, into=parity)
             leg("a2a", parity_sharded, dev, ws, rank, "a2a", into=parity)
             if ws > 1:
-                leg("dropin_exchanges", parity_dropin_exchanges, dev, ws, rank, into=parity)
                 if es is not None:
                     nt = len(es.params())
                     leg(f"bf16_{es.name}", codec_parity, es, dev, ws, rank, cap,

@@ -229,7 +229,8 @@ class TrainingComm:
     """src/comm.py:71-149. `transport` (default: DILOCO_P2P_TRANSPORT, else "host") selects the
     pipeline p2p threads: "host" = the reference's (frame, copy to host, gloo send/recv);
     "device" = p2p.DeviceSendThread / DeviceRecvThread (GPU framing, header over the same gloo
-    group, payload over per-direction RCCL data groups)."""
+    group, payload over per-direction RCCL data groups) on `device`
+    (default cuda:world.local_rank, the device src/train.py:368 trains on)."""
 
     def __init__(self, world, shape: Tuple[int, ...], logger, transport: Optional[str] = None,
                  device: Optional[torch.device] = None, serializer_factory=None):
@@ -248,8 +249,9 @@ class TrainingComm:
         elif self.transport == "device":
             from .p2p import DeviceRecvThread, DeviceSendThread, boundary_data_groups
 
-            if device is None:
-                device = torch.device("cuda", torch.cuda.current_device())
+            if device is None:  # the reference's device: cuda:local_rank (src/utils.py:36-40,
+                # src/train.py:368), not the current device, which it never sets
+                device = torch.device("cuda", world.local_rank)
             if serializer_factory is not None:
                 kw["serializer"] = serializer_factory(shape)
             dg = self.data_groups = boundary_data_groups(world)

@@ -577,7 +577,10 @@ class DeviceOuterMirror:
 
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
                  bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = False,
-                 wire: str = "f32", exchange: str = "sharded"):
+                 wire: str = "f32", exchange: str = "sharded", keep_params: bool = False):
+        """keep_params: the outer model's Parameter objects stay the ones it has (their class
+        switched to OuterParameter in place) -- for an outer model that got its device only
+        at its first compute_pseudo_gradient, after get_optimizer took references to them."""
         if wire not in OUTER_WIRES:
             raise ValueError(f"wire {wire!r}: one of {OUTER_WIRES}")
         if exchange not in OUTER_EXCHANGES:
@@ -621,9 +624,12 @@ class DeviceOuterMirror:
         self.theta_touched = True
         self.grads_touched = True
         self._theta_ver = None
+        # the outer parameters share d_theta's version counter (OuterParameters made over its
+        # views): θ's version is one integer; parameters kept in place keep their own counters
+        self._shared_ver = fused and not keep_params
         self._relay_theta()
         if fused:
-            self._install_outer_parameters(outer_model)
+            self._install_outer_parameters(outer_model, keep_params)
         self._delta = None   # pending pseudo-gradient: (inner params, ptrs, versions, θ versions)
         self._div = 1        # pending /n: d_wire holds the Σ of the peers' deltas
         self._target = None  # (inner params, ptrs, versions) of the last compute_pseudo_gradient
@@ -652,15 +658,22 @@ class DeviceOuterMirror:
     def __reduce_ex__(self, proto):  # ... and so does a pickled one
         return (_none, ())
 
-    def _install_outer_parameters(self, model: torch.nn.Module) -> None:
+    def _install_outer_parameters(self, model: torch.nn.Module, keep: bool = False) -> None:
         """Fused mode: every parameter of the outer model becomes an OuterParameter created
         over its view of the θ arena (shared parameters stay shared). A tensor made from a view
         shares its base's version counter, so every in-place write to any outer parameter
         bumps d_theta's one counter: the per-call check that θ is unchanged reads one integer
-        instead of 148 (or 292) version counters."""
+        instead of 148 (or 292) version counters. keep: the same Parameter objects, their class
+        switched in place (their data already are the arena's views, _relay_theta)."""
+        ref = weakref.ref(self)
+        if keep:
+            for p in self.params:
+                p.__class__ = OuterParameter
+                p.__dict__["_dl_mirror"] = ref
+            self._theta_ver = self._theta_version()
+            return
         index = {id(p): i for i, p in enumerate(self.params)}
         new: List[Optional[OuterParameter]] = [None] * len(self.params)
-        ref = weakref.ref(self)
         for mod in model.modules():
             for name, p in list(mod._parameters.items()):
                 if p is None:
@@ -676,8 +689,8 @@ class DeviceOuterMirror:
 
     def _theta_version(self):
         """fused: d_theta's version counter, shared by every outer parameter (one integer);
-        eager: the parameters' own counters."""
-        return self.d_theta._version if self.fused else _vers(self.params)
+        eager, or parameters kept in place: the parameters' own counters."""
+        return self.d_theta._version if self._shared_ver else _vers(self.params)
 
     def _make_views(self, arena: torch.Tensor) -> List[torch.Tensor]:
         return [arena[o:o + n].view(p.shape)

@@ -34,8 +34,11 @@ import torch.distributed as dist
 
 from .serializer import Metadata, Serializer
 
-# payload backend of the device transport: "nccl" (RCCL) or "gloo" (host-staged, tests)
-P2P_BACKEND = os.environ.get("DILOCO_P2P_BACKEND", "nccl")
+
+def p2p_backend() -> str:
+    """Payload backend of the device transport, read when the groups are made:
+    DILOCO_P2P_BACKEND, "nccl" (RCCL) by default or "gloo" (host-staged, tests)."""
+    return os.environ.get("DILOCO_P2P_BACKEND", "nccl")
 
 
 def _staged(group) -> bool:
@@ -164,7 +167,7 @@ def boundary_data_groups(world, backend: str = None) -> Dict[Tuple[int, int, str
     """One forward and one backward data group per stage boundary (s, s+1), over the same
     ranks as the reference's world.local_pg[(s, s+1)]. Collective: every rank calls it, in
     the same order (TrainingComm.__init__ runs on every rank)."""
-    backend = backend or P2P_BACKEND
+    backend = backend or p2p_backend()
     groups = {}
     for s in range(world.num_stages - 1):
         ranks = sorted(world.stage2ranks[s] + world.stage2ranks[s + 1])

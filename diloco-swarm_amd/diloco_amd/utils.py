@@ -66,6 +66,7 @@ _WRITE_BACK = "_diloco_write_back"
 _FUSED = "_diloco_fused"
 _WIRE = "_diloco_wire"
 _EXCHANGE = "_diloco_exchange"
+_PENDING = "_diloco_pending_device"  # placement="device" built before the inner model moved
 PLACEMENTS = ("host", "device")
 _TRUE = ("1", "true", "on", "yes")
 _FALSE = ("0", "false", "off", "no")
@@ -106,11 +107,21 @@ def outer_mirror(outer_model: nn.Module, device=None):
             p = next(outer_model.parameters(), None)
             if p is None:
                 raise ValueError("outer model has no parameters")
+            keep = getattr(outer_model, _PENDING, False)
+            dev = p.device
+            if keep:  # the device is the inner model's, named now by the caller
+                if device is None:
+                    raise RuntimeError("the device outer model gets its device from the inner "
+                                       "model's first compute_pseudo_gradient on the GPU")
+                dev = torch.device(device)
+                _move_params(outer_model, dev)
+                object.__setattr__(outer_model, _PENDING, False)
             cap = int(os.environ.get("DILOCO_OUTER_BUCKET_ELEMS", DEFAULT_BUCKET_CAP_ELEMS))
-            m = DeviceOuterMirror(outer_model, p.device, kernels=k, bucket_cap_elems=cap,
+            m = DeviceOuterMirror(outer_model, dev, kernels=k, bucket_cap_elems=cap,
                                   fused=getattr(outer_model, _FUSED, False),
                                   wire=getattr(outer_model, _WIRE, "f32"),
-                                  exchange=getattr(outer_model, _EXCHANGE, "sharded"))
+                                  exchange=getattr(outer_model, _EXCHANGE, "sharded"),
+                                  keep_params=keep)
             object.__setattr__(outer_model, _ATTR, m)
             return m
         if device is None:
@@ -131,6 +142,16 @@ def outer_mirror(outer_model: nn.Module, device=None):
             m = HostOuterMirror(outer_model, torch.device(device), kernels=k, write_back=wb)
         object.__setattr__(outer_model, _ATTR, m)  # not a submodule / not in state_dict
     return m
+
+
+def _move_params(model: nn.Module, device: torch.device) -> None:
+    """Every parameter (and gradient) of `model` onto `device`, the Parameter objects kept
+    (an optimizer built on them stays valid)."""
+    with torch.no_grad():
+        for p in module_params(model):
+            p.data = p.data.to(device)
+            if p.grad is not None:
+                p.grad = p.grad.to(device)
 
 
 def _inner_device(inner_model: nn.Module) -> torch.device:
@@ -175,23 +196,26 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     has_params = next(inner_model.parameters(), None) is not None
     if placement == "host":
         outer_model = outer_model.to("cpu")
-    elif has_params:  # the inner model's GPU; the reference builds the outer model before moving the
-        # inner one (src/train.py:382), so a CPU inner model means the current device
+    elif has_params:  # the inner model's GPU. The reference builds the outer model before it
+        # moves the inner one to cuda:local_rank (src/train.py:382, :163, :368 with
+        # src/utils.py:36-40) and never sets the current device: a CPU inner model leaves the
+        # outer one on the CPU until the first compute_pseudo_gradient names the device
+        # (outer_mirror; until then the four calls are the reference's host loops)
         dev = _inner_device(inner_model)
-        if dev.type == "cpu":
-            dev = getattr(default_kernels(), "default_device", None)
-            if dev is None:
-                if not torch.cuda.is_available():
-                    raise RuntimeError("placement='device' needs a HIP device")
-                dev = torch.device("cuda", torch.cuda.current_device())
-        outer_model = outer_model.to(dev)
+        if dev.type == "cpu" and device_path(next(inner_model.parameters())):
+            # a test backend that computes on host tensors (tests/oracle_kernels.py)
+            outer_model = outer_model.to(default_kernels().default_device)
+        elif dev.type == "cpu":
+            object.__setattr__(outer_model, _PENDING, True)
+        else:
+            outer_model = outer_model.to(dev)
     object.__setattr__(outer_model, _OUTER, True)  # get_optimizer: SGD here is the outer SGD
     object.__setattr__(outer_model, _PLACEMENT, placement)
     object.__setattr__(outer_model, _WRITE_BACK, write_back)
     object.__setattr__(outer_model, _FUSED, bool(fused) and lazy)
     object.__setattr__(outer_model, _WIRE, wire)
     object.__setattr__(outer_model, _EXCHANGE, exchange)
-    if placement == "device" and has_params:
+    if placement == "device" and has_params and not getattr(outer_model, _PENDING, False):
         # lay the parameters out in the packed HBM arena now (fused: as OuterParameters);
         # a model without parameters keeps none: the four calls are the reference's empty loops
         outer_mirror(outer_model)

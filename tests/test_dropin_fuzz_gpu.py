@@ -110,7 +110,7 @@ def _run_case(case, rank, world, dev):
     opt = get_optimizer(outer, _Cfg(type="SGD", lr=c["lr"], momentum=momentum,
                                     nesterov=nesterov))
     comm = TrainingComm(World.from_default_group(1), (1, 1, 8), None)
-    m = outer_mirror(outer)
+    m = outer_mirror(outer, dev)  # the device outer model takes the inner model's device
     tree = getattr(m, "dev", m).tree
     st = oracle.OuterState(c["theta0"], lr=c["lr"], momentum=momentum, nesterov=nesterov)
     exact = c["exchange"] in ("a2a", "int8")

@@ -70,7 +70,10 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
     deferred = write_back == "deferred"
     inner = inner.to("cuda:0")
     if placement == "device":
-        assert all(p.is_cuda for p in outer.parameters())
+        # built while the inner model was on the CPU: the outer model waits for the first
+        # compute_pseudo_gradient to name its device (never the current device, which the
+        # reference does not set); the optimizer below is built on these very Parameters
+        assert not any(p.is_cuda for p in outer.parameters())
     if stock_sgd:
         opt = torch.optim.SGD(outer.parameters(), lr=0.7, momentum=0.9, nesterov=True)
     else:
@@ -88,6 +91,10 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
         # tensors only after sync_inner_model's write-back (waited for by the flush)
         mid = not quiet and (not deferred or s == 1)
         compute_pseudo_gradient(inner, outer)
+        if placement == "device":  # the same Parameter objects, now in the inner model's HBM
+            assert all(p.device == torch.device("cuda", 0) for p in outer.parameters())
+            assert all(map(lambda a, b: a is b, opt.param_groups[0]["params"],
+                           outer.parameters()))
         if deferred and mid:
             flush_outer_model(outer)
         if mid:

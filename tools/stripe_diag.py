@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Localise the config #5 wrong-sum flake on the ranks themselves.
+
+The round-4 records (profiles/r04_fence_probe_{a,b}.txt) pin its shape: in every failure one
+rank's contribution is exactly zero on every element of the 256-element blocks whose index is
+p mod 8 (k such phases for a k-fold failure) -- the blocks the test's input generator
+dl_fill_synth (4096 workgroups, 256 elements per workgroup per grid-stride step) writes from
+the workgroups with id = p mod 8, i.e. from one XCD. A zero delta means the pack read the inner
+parameters as they were before that fill (θ, since the inner model equals the outer one after
+sync_inner_model). This tool runs the same eight-process config #5 sequence (gloo, one GPU,
+the reference's four calls, no host wait before the collectives) and, per rank and step:
+
+  pack      snapshot of the bf16 wire right after pack(b) (a clone on the same stream)
+  inner_q   snapshot of the inner window taken right after pack(b) on the same stream
+  inner_h   the inner window read after a host synchronize once sync_gradients returned
+
+each compared with the fill's exact output; mismatching 256-element blocks are reported by
+phase (block index mod 8). pack stale + inner_h fresh = the pack read before the fill's stores
+were visible (late); inner_h stale too = the stores never landed (lost).
+
+    python tools/stripe_diag.py RUNS [MAX_FAILS]
+"""
+import os
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(HERE, "tests"), HERE, os.path.join(HERE, "diloco-swarm_amd")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+WIN = [(0, 37_000_011, 4 << 20), (1, 0, 2 << 20)]  # (tensor, first element, count), as the test
+
+
+def _bf16_bits(x32):
+    """fp32 -> bf16 bits, round to nearest even (torch's .to(bfloat16))."""
+    return torch.from_numpy(np.ascontiguousarray(x32)).to(torch.bfloat16).view(torch.int16).numpy()
+
+
+def _phases(bad_idx, lo):
+    if bad_idx.size == 0:
+        return None
+    blocks = np.unique((lo + bad_idx) // 256)
+    return {"n": int(bad_idx.size), "blocks": int(blocks.size),
+            "phase": np.bincount(blocks % 8, minlength=8).tolist()}
+
+
+def _worker(rank, world, port, out):
+    os.environ["DILOCO_DP_BACKEND"] = "gloo"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    from diloco_amd import mirror, staging, synth
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+    from test_dropin_gpu import SGD_CFG
+
+    def no_wait(group, t):
+        return None
+    staging.before_collective = no_wait
+    mirror.before_collective = no_wait
+
+    snaps = {}
+    orig = mirror.DeviceOuterMirror._launch_reductions
+
+    def launch(self, pack, view, group):
+        inner = self._target[0] if self._target is not None else None
+
+        def pack2(b):
+            pack(b)
+            for t, lo, m in WIN:
+                o = self.offs[t]
+                blo, bhi = self.tree.bucket_ranges[b]
+                if blo <= o < bhi:
+                    snaps[("pack", t)] = self.d_wire16[o + lo:o + lo + m].clone()
+                    snaps[("inner_q", t)] = inner[t].detach().view(-1)[lo:lo + m].clone()
+                    snaps[("theta", t)] = self.d_theta[o + lo:o + lo + m].clone()
+        return orig(self, pack2 if pack is not None else None, view, group)
+    mirror.DeviceOuterMirror._launch_reductions = launch
+
+    spec = get_tree("t1.3b")
+    shapes = [sh for _, sh in spec.params()]
+    inner = torch.nn.Module()
+    inner.ps = torch.nn.ParameterList(
+        [torch.nn.Parameter(x.view(sh)) for x, sh in zip(synth.outer_tree_device(spec, "cuda:0"),
+                                                          shapes)])
+    outer = get_outer_model(inner, "device", wire="bf16")
+    opt = get_optimizer(outer, SGD_CFG)
+    comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
+    ops, ips = list(outer.parameters()), list(inner.parameters())
+    rec = {}
+    for s in (1, 2):
+        snaps.clear()
+        th = [p.detach().view(-1) for p in ops]
+        synth.inner_tree_device(th, s, rank, out=[p.data.view(-1) for p in ips])
+        compute_pseudo_gradient(inner, outer)
+        comm.sync_gradients(outer)
+        torch.cuda.synchronize()
+        inner_h = {t: ips[t].detach().view(-1)[lo:lo + m].cpu().numpy() for t, lo, m in WIN}
+        opt.step()
+        sync_inner_model(outer, inner)
+        torch.cuda.synchronize()
+        for t, lo, m in WIN:
+            theta = snaps[("theta", t)].cpu().numpy()
+            u = synth.uniform(synth.noise_seed(s, rank), t, m, start=lo)
+            want_inner = (np.float32(0.0) + u * np.float32(synth.NOISE_SCALE)) + theta
+            want_inner = want_inner.astype(np.float32)
+            want_pack = _bf16_bits((theta - want_inner).astype(np.float32))
+            got_pack = snaps[("pack", t)].view(torch.int16).cpu().numpy()
+            got_q = snaps[("inner_q", t)].cpu().numpy()
+            r = {"pack": _phases(np.flatnonzero(got_pack != want_pack), lo),
+                 "pack_zero": int(np.count_nonzero((got_pack == 0) & (want_pack != 0))),
+                 "inner_q": _phases(np.flatnonzero(got_q != want_inner), lo),
+                 "inner_q_is_theta": int(np.count_nonzero((got_q == theta) & (want_inner != theta))),
+                 "inner_h": _phases(np.flatnonzero(inner_h[t] != want_inner), lo),
+                 "inner_h_is_theta": int(np.count_nonzero((inner_h[t] == theta)
+                                                          & (want_inner != theta)))}
+            if any(r[k] for k in ("pack", "inner_q", "inner_h")):
+                rec[f"s{s}_t{t}"] = r
+    np.save(os.path.join(out, f"r{rank}.npy"), np.array([repr(rec)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    import test_dropin_gpu as t
+
+    runs = int(sys.argv[1])
+    max_fails = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    fails = 0
+    for i in range(runs):
+        t0 = time.time()
+        out = tempfile.mkdtemp()
+        mp.spawn(_worker, args=(8, t._free_port(), out), nprocs=8, join=True)
+        recs = {r: str(np.load(os.path.join(out, f"r{r}.npy"))[0]) for r in range(8)}
+        bad = {r: v for r, v in recs.items() if v != "{}"}
+        print(i, f"{time.time() - t0:.0f}s", bad if bad else "clean", flush=True)
+        fails += bool(bad)
+        if fails >= max_fails:
+            break
