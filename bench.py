@@ -244,17 +244,24 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
     inner, outer, opt, comm = _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange,
                                               placement)
 
+    issue, wait = [], []  # synced: per step, the four calls' host time and the synchronize's
+
     def one():
+        t1 = time.perf_counter()
         compute_pseudo_gradient(inner, outer)
         comm.sync_gradients(outer)
         opt.step()
         sync_inner_model(outer, inner)
         if synced:
+            t2 = time.perf_counter()
             torch.cuda.synchronize()
+            issue.append(t2 - t1)
+            wait.append(time.perf_counter() - t2)
 
     for _ in range(max(warmup, 1)):
         one()
     _sync(ws)
+    del issue[:], wait[:]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
     ev[0].record()
@@ -281,7 +288,8 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
            "value_aggregate": ws * 4.0 * P / dt / 1e9, "loop_gpu_ms_per_step": round(loop_ms, 5),
            "wire": wire, "exchange": ex if ws > 1 else "none (one peer)",
            "hbm_bytes_per_param": round(bpp, 3), "synced": synced,
-           **({"mean_ms_per_step": round(mean_ms, 5), "timing": "median step (synced)"}
+           **({"mean_ms_per_step": round(mean_ms, 5), "timing": "median step (synced)",
+               "steps_ms": _spread(per), "issue_ms": _spread(issue), "sync_wait_ms": _spread(wait)}
               if synced else {}),
            "placement": ("device" if mm is m else "host (write_back lazy: HBM twin)")}
     if ws == 1:
@@ -310,6 +318,16 @@ def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None
     del outer, opt, inner, m, mm
     torch.cuda.empty_cache()
     return res
+
+
+def _spread(xs):
+    """Median, mean, p90, max and the five slowest of a list of seconds, in ms."""
+    if not xs:
+        return None
+    a = np.sort(np.asarray(xs) * 1e3)
+    return {"median": round(float(np.median(a)), 4), "mean": round(float(a.mean()), 4),
+            "p90": round(float(a[int(0.9 * (len(a) - 1))]), 4), "max": round(float(a[-1]), 4),
+            "slowest": [round(float(x), 3) for x in a[-5:][::-1]]}
 
 
 def exchange_roofline(m, ws, dev, steps, group):
@@ -1143,6 +1161,8 @@ def leg_summary(r):
         s["frac"] = _r(roof.get("frac"))
     if "ms_per_step" in r:
         s["ms"] = _r(r["ms_per_step"], 4)
+    if "mean_ms_per_step" in r:  # a median-timed leg: its mean beside it
+        s["mean_ms"] = _r(r["mean_ms_per_step"], 4)
     if "hbm_bytes_per_param" in r:
         s["Bpp"] = r["hbm_bytes_per_param"]
     return s
@@ -1437,12 +1457,10 @@ def main():
                 # first: the north star's N > 1 figure -- the 1.3B bucket set through the calls
                 # against RCCL's own all_reduce of the same bytes, this node, this run
                 ks = max(3, a.steps // 4)
-                # the 1.3B legs at N > 1 keep the outer model in HBM: the host placement's CPU
-                # copy (θ, .grad, momentum: 15.8 GB of host memory per rank, as the
-                # reference's own CPU outer model) times eight ranks is what a node's RAM
-                # holds only if nothing else does; the kernels and the exchange are the same
-                r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1, "f32", None,
-                          "sharded", False, False, "device")
+                # get_outer_model's default placement, as the headline: the CPU outer model
+                # holds 4 B/param resident per rank (its θ; the pageable .grad / momentum
+                # arenas fill only when read), 5.3 GB at 1.3B
+                r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1)
                 ref13 = leg(f"rccl_ref_{es.name}", rccl_reference, dev, ws, rank,
                             es.total() // (64 * ws) * (64 * ws), 3, into=em.detail)
                 e = exchange_efficiency(r13, ref13, ws)
@@ -1459,10 +1477,8 @@ def main():
             leg(f"{spec.name}_engine", run_engine, spec, dev, ws, rank, a.steps, a.warmup,
                 torch.float32, cap)
             if es is not None:
-                leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16", None,
-                    "sharded", False, False, "device")
-                leg(f"{es.name}_dropin_int8", run_dropin, es, dev, ws, rank, ks, 1, "int8", None,
-                    "sharded", False, False, "device")
+                leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16")
+                leg(f"{es.name}_dropin_int8", run_dropin, es, dev, ws, rank, ks, 1, "int8")
             leg(f"{spec.name}_grad_sync", gradsync_rate, spec, dev, ws, rank, max(3, a.steps // 2))
             if ws >= 4 and ws % 2 == 0:
                 leg(f"{spec.name}_two_stages", run_two_stages, spec, dev, ws, rank, a.steps,

@@ -892,4 +892,10 @@ DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_i
   return e == hipSuccess ? DL_OK : hip_fail(e, "dl_fill_synth");
 }
 
+DL_API int dl_spin(uint64_t ns, dl_stream_t s) {
+  if (ns > 10000000000ull) return fail(DL_E_ARG, "dl_spin: %llu ns > 10 s", (unsigned long long)ns);
+  hipError_t e = dl::launch_spin(ns, static_cast<hipStream_t>(s));
+  return e == hipSuccess ? DL_OK : hip_fail(e, "dl_spin");
+}
+
 }  // extern "C"

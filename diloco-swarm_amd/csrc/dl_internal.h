@@ -87,6 +87,7 @@ hipError_t launch_serialize(const void* src, int src_dtype, int64_t numel, float
                             float* out, hipStream_t s);
 hipError_t launch_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id,
                              float base, float scale, const float* add, hipStream_t s);
+hipError_t launch_spin(uint64_t ns, hipStream_t s);
 // dl_tree_bind: out[c] = segptr[chunks[c].seg] + 4 * loff[c] for every chunk c
 hipError_t launch_resolve_chunks(const Chunk* chunks, const int64_t* loff, const uint64_t* segptr,
                                  int32_t nch, void** out, hipStream_t s);

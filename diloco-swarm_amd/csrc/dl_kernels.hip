@@ -971,11 +971,32 @@ hipError_t launch_serialize_f64(const double* src, int64_t numel, float m0, floa
   return hipGetLastError();
 }
 
+// the device wall clock (100 MHz on MI355X; the launcher converts with the reported rate)
+__global__ void __launch_bounds__(64) k_spin(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+hipError_t launch_spin(uint64_t ns, hipStream_t s) {
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess) return e;
+  const uint64_t ticks = ns * uint64_t(khz > 0 ? khz : 100000) / 1000000ull;
+  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id, float base,
                              float scale, const float* add, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const uint64_t key0 = seed * 0xD1B54A32D192ED03ull + (stream_id << 40);
-  hipLaunchKernelGGL(k_fill_synth, dim3(grid_for(n)), dim3(kThreads), 0, s, dst, n, key0, base,
+  // one workgroup per 256 elements (the grid-stride loop only past 2^38 elements): short-lived
+  // workgroups like the outer-step kernels' (with eight processes time-sharing the
+  // GPU, a long-lived grid-stride fill lost one XCD's share of its stores)
+  int64_t g = (n + kThreads - 1) / kThreads;
+  if (g > (1ll << 30)) g = 1ll << 30;
+  hipLaunchKernelGGL(k_fill_synth, dim3(unsigned(g)), dim3(kThreads), 0, s, dst, n, key0, base,
                      scale, add);
   return hipGetLastError();
 }

@@ -84,6 +84,7 @@ SIGNATURES = {
     "dl_serialize": (ctypes.c_int, [_vp, _i32, _i64, _f32, _f32, _vp, _vp]),
     "dl_serialize_f64": (ctypes.c_int, [_vp, _i64, _f32, _f32, _vp, _vp]),
     "dl_fill_synth": (ctypes.c_int, [_vp, _i64, _u64, _u64, _f32, _f32, _vp, _vp]),
+    "dl_spin": (ctypes.c_int, [_u64, _vp]),
     "dl_rccl_load": (ctypes.c_int, [ctypes.c_char_p]),
     "dl_rccl_version": (ctypes.c_int, [_pi32]),
     "dl_comm_unique_id": (ctypes.c_int, [_vp]),

@@ -27,7 +27,6 @@ from .kernels import default_kernels
 from . import _lib
 from .outer import _Done, pipelined_buckets
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_GRAD
-from .staging import before_collective, collective
 
 
 class GradSync:
@@ -108,9 +107,8 @@ class GradSync:
         pipelined_buckets(
             self.tree.n_buckets,
             lambda b: self.k.gather(self.tree, b, SLOT_GRAD, self.wire),
-            lambda b: _Done() if local else collective(
-                dist.all_reduce, self.group, view(b), op=dist.ReduceOp.SUM, group=self.group,
-                async_op=True),
+            lambda b: _Done() if local else dist.all_reduce(
+                view(b), op=dist.ReduceOp.SUM, group=self.group, async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, self.wire, self.world_size, SLOT_GRAD),
         )
 
@@ -126,7 +124,6 @@ class GradSync:
         def a2a(b):
             lo, hi = self.tree.bucket_ranges[b]
             self.k.gather(self.tree, b, SLOT_GRAD, self.wire)
-            before_collective(self.group, self.wire)
             return dist.all_to_all_single(self.a2a_recv[b % 2][:n * shard(b)], self.wire[lo:hi],
                                           group=self.group, async_op=True)
 
@@ -141,7 +138,6 @@ class GradSync:
             s = shard(b)
             self.k.shard_reduce_avg(self.a2a_recv[b % 2][:n * s], n, self.a2a_avg[b % 2][:s])
             lo, hi = self.tree.bucket_ranges[b]
-            before_collective(self.group, self.a2a_avg[b % 2])
             ag[b] = dist.all_gather_into_tensor(self.wire[lo:hi], self.a2a_avg[b % 2][:s],
                                                 group=self.group, async_op=True)
             if b >= 1:

@@ -42,7 +42,6 @@ from . import _lib
 from .kernels import default_kernels
 from .outer import pipelined_buckets
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_GRAD, SLOT_INNER
-from .staging import before_collective, collective
 
 ALL = _lib.ALL_BUCKETS
 S_CHUNK = _lib.CHUNK_ELEMS  # elements per tree chunk (one int8 slot each)
@@ -80,10 +79,8 @@ def ordered_average(k, tree, wire: torch.Tensor, recv: torch.Tensor, group, n: i
     landing buffer the wire's size."""
     for lo, hi in tree.bucket_ranges:
         s = (hi - lo) // n
-        before_collective(group, wire)
         dist.all_to_all_single(recv[lo:hi], wire[lo:hi], group=group)
         k.shard_reduce_avg(recv[lo:hi], n, wire[lo + rank * s:lo + (rank + 1) * s])
-        before_collective(group, wire)
         dist.all_gather_into_tensor(wire[lo:hi], wire[lo + rank * s:lo + (rank + 1) * s],
                                     group=group)
 
@@ -293,8 +290,8 @@ class HostOuterMirror:
 
         pipelined_buckets(
             self.tree.n_buckets, lambda b: None,
-            lambda b: collective(dist.all_reduce, group, view(b), op=dist.ReduceOp.SUM,
-                                  group=group, async_op=True),
+            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group,
+                                      async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
         )
         self._grads_to_host()
@@ -804,7 +801,6 @@ class DeviceOuterMirror:
             a, e = self._own(b, n, r)
             if mode == "a2a":
                 self.k.shard_reduce_avg(self.d_recv[lo:hi], n, self.d_wire[a:e])
-            before_collective(g, self.d_wire)
             dist.all_gather_into_tensor(self.d_wire[lo:hi], self.d_wire[a:e], group=g)
 
     def gather_momentum(self) -> None:
@@ -817,7 +813,6 @@ class DeviceOuterMirror:
         for b in range(self.tree.n_buckets):
             lo, hi = self.tree.bucket_ranges[b]
             a, e = self._own(b, n, r)
-            before_collective(g, self.d_mom)
             dist.all_gather_into_tensor(self.d_mom[lo:hi], self.d_mom[a:e], group=g)
 
     def _sharded_sgd(self, mom, lr, momentum, nesterov, first, target) -> None:
@@ -841,7 +836,6 @@ class DeviceOuterMirror:
                 self.k.shard_reduce_avg(self.d_recv[lo:hi], n, self.d_wire[a:e])
             self.k.shard_sgd(self.d_wire[a:e], 1 if mode == "a2a" else n, self.d_theta[a:e],
                              None if mom is None else mom[a:e], lr, momentum, nesterov, first)
-            before_collective(g, self.d_theta)
             ags[b] = dist.all_gather_into_tensor(self.d_theta[lo:hi], self.d_theta[a:e],
                                                  group=g, async_op=True)
             if b >= 1:
@@ -972,8 +966,8 @@ class DeviceOuterMirror:
             return
         pipelined_buckets(
             self.tree.n_buckets, pack or (lambda b: None),
-            lambda b: collective(dist.all_reduce, group, view(b), op=dist.ReduceOp.SUM,
-                                  group=group, async_op=True),
+            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group,
+                                      async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, self.d_wire, num_peers, -1, self.d_wire),
         )
 
@@ -1010,8 +1004,8 @@ class DeviceOuterMirror:
             return
         pipelined_buckets(
             self.tree.n_buckets, pack,
-            lambda b: collective(dist.all_reduce, group, view(b), op=dist.ReduceOp.SUM,
-                                  group=group, async_op=True),
+            lambda b: dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group,
+                                      async_op=True),
             lambda b: self.k.unpack_avg(self.tree, b, w16, num_peers, -1, self.d_wire),
         )
 
@@ -1045,7 +1039,6 @@ class DeviceOuterMirror:
                 pack(b)
             lo, hi = self.tree.bucket_ranges[b]
             a, e = self._own(b, n, rank)
-            before_collective(group, self.d_wire)
             if mode == "a2a":
                 works.append(dist.all_to_all_single(self.d_recv[lo:hi], self.d_wire[lo:hi],
                                                     group=group, async_op=True))
@@ -1120,7 +1113,6 @@ class DeviceOuterMirror:
 
         def a2a(b):
             nch, m, _, _ = q["plan"][b]
-            before_collective(group, q["recv"][b % 2])
             return dist.all_to_all_single(q["recv"][b % 2][:n * m * S], self._q8_region(q, b),
                                           group=group, async_op=True)
 
@@ -1135,7 +1127,6 @@ class DeviceOuterMirror:
             nch, m, _, rb = q["plan"][b]
             red = q["red"][rb * S:(rb + m) * S]
             self.k.q8_reduce(q["recv"][b % 2][:n * m * S], n, m, n, red)
-            before_collective(group, red)
             works[b] = dist.all_gather_into_tensor(self._q8_region(q, b), red, group=group,
                                                    async_op=True)
         self._works = works
@@ -1186,7 +1177,6 @@ class DeviceOuterMirror:
         for b in range(self.tree.n_buckets):
             if pack is not None:
                 pack(b)
-            before_collective(group, view(b))
             works.append(dist.all_reduce(view(b), op=dist.ReduceOp.SUM, group=group,
                                          async_op=True))
         self._works = works
@@ -1487,13 +1477,15 @@ class LazyHostOuterMirror:
         self._twin = twin
         self.fused, self.wire, self.exchange = fused, wire, exchange
         self.tree, self.offs, self.numels = self.dev.tree, self.dev.offs, self.dev.numels
-        # pinned host arenas: one async DMA per read (pageable arenas measured the same for the
-        # step itself, profiles/r04_placement_ab_order.txt)
-        pin = self.device.type == "cuda"
-        z = dict(dtype=torch.float32, pin_memory=pin)
-        self.h = {"theta": torch.zeros(self.tree.total, **z),
-                  "grad": torch.zeros(self.tree.total, **z), "mom": None}
-        self._pin = pin
+        # host arenas, pageable by default: pinned and pageable measured the same for the step
+        # (profiles/r04_placement_ab_order.txt) -- nothing crosses PCIe unless the host reads --
+        # and pageable pages of the .grad / momentum arenas are not resident until a read
+        # fills them (4 B/param resident per rank instead of 12 pinned).
+        # DILOCO_HOST_PIN=1 pins them (one async DMA per read)
+        from .utils import env_flag
+
+        self._pin = self.device.type == "cuda" and env_flag("DILOCO_HOST_PIN", False)
+        self.h = {"theta": self._arena(zero=True), "grad": self._arena(), "mom": None}
         ref = weakref.ref(self)
         with _NO_TF(), torch.no_grad():
             self._theta_views = self._views(self.h["theta"])
@@ -1512,6 +1504,20 @@ class LazyHostOuterMirror:
         self._written: set = set()  # arenas written on the host since the last upload
         self._grads_set = False  # the API .grads are the grad arena's views
         self.theta_touched = self.grads_touched = False
+
+    def _arena(self, zero: bool = False) -> torch.Tensor:
+        """A host arena of the packed layout. Not zero: left unwritten (pageable pages stay
+        unresident until a read from HBM fills the arena) except the alignment gaps between
+        segments, zeroed so that an upload of the arena never carries garbage into HBM."""
+        z = dict(dtype=torch.float32, pin_memory=self._pin)
+        if zero:
+            return torch.zeros(self.tree.total, **z)
+        a = torch.empty(self.tree.total, **z)
+        ends = [o + n for o, n in zip(self.offs, self.numels)]
+        for e, o in zip(ends, self.offs[1:] + [self.tree.total]):
+            if o > e:
+                a[e:o].zero_()
+        return a
 
     def _views(self, arena: torch.Tensor) -> List[torch.Tensor]:
         return [arena[o:o + n].view(p.shape)
@@ -1650,8 +1656,7 @@ class LazyHostOuterMirror:
         if momentum == 0:
             return [None] * len(self.params)
         if self._mom_views is None:
-            self.h["mom"] = torch.zeros(self.tree.total, dtype=torch.float32,
-                                        pin_memory=self._pin)
+            self.h["mom"] = self._arena()
             self._mom_views = [self._host_tensor(v, "mom") for v in self._views(self.h["mom"])]
             self._ver["mom"] = self.h["mom"]._version
         self._dirty.add("mom")

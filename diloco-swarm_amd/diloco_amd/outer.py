@@ -41,7 +41,6 @@ import torch.distributed as dist
 from . import _lib
 from .kernels import Q8_SLOT, default_kernels
 from .plan import DEFAULT_BUCKET_CAP_ELEMS, SLOT_INNER
-from .staging import before_collective
 
 ALL = _lib.ALL_BUCKETS
 # Tile of dl_pack_sgd_tiled: 8192 chunks = 32 Mi elements, 128 MiB per stream (wire + θ of a
@@ -316,11 +315,9 @@ class OuterSync:
         n = self.world_size
         region = self.q8_region(bucket)
         recv = self.q_recv[:n * m * Q8_SLOT]
-        before_collective(self.group, region)
         dist.all_to_all_single(recv, region, group=self.group, async_op=True).wait()
         red = self.q_red[:m * Q8_SLOT]
         self.k.q8_reduce(recv, n, m, n, red)
-        before_collective(self.group, red)
         return dist.all_gather_into_tensor(region, red, group=self.group, async_op=True)
 
     # ---- sharded variant --------------------------------------------------------
@@ -366,13 +363,11 @@ class OuterSync:
         if self.a2a:
             if self._local():  # one replica: the bucket itself is the one slice
                 return _Done()
-            before_collective(self.group, self.bucket_view(bucket))
             return dist.all_to_all_single(self._a2a_slices(bucket), self.bucket_view(bucket),
                                           group=self.group, async_op=async_op)
         if self._local():
             self._shard(self.g_shard, bucket).copy_(self.bucket_view(bucket))
             return _Done()
-        before_collective(self.group, self.bucket_view(bucket))
         return dist.reduce_scatter_tensor(self._shard(self.g_shard, bucket),
                                           self.bucket_view(bucket), op=dist.ReduceOp.SUM,
                                           group=self.group, async_op=async_op)
@@ -395,7 +390,6 @@ class OuterSync:
         if self._local():
             self.theta[lo:hi].copy_(self.th_shard_view(bucket))
             return _Done()
-        before_collective(self.group, self.theta)
         return dist.all_gather_into_tensor(self.theta[lo:hi], self.th_shard_view(bucket),
                                            group=self.group, async_op=async_op)
 
@@ -411,7 +405,6 @@ class OuterSync:
                 return None
             out = torch.empty(self.tree.total, dtype=torch.float32, device=self.device)
             if self.world_size > 1:
-                before_collective(self.group, out)
                 dist.all_gather_into_tensor(out, self.mom_x, group=self.group)
             else:
                 out.copy_(self.mom_x)
@@ -424,7 +417,6 @@ class OuterSync:
             if self._local():
                 out[lo:hi].copy_(self._shard(self.mom_shard, b))
             else:
-                before_collective(self.group, out)
                 dist.all_gather_into_tensor(out[lo:hi], self._shard(self.mom_shard, b),
                                             group=self.group)
         return out
@@ -446,7 +438,6 @@ class OuterSync:
     def all_reduce(self, bucket: int, async_op: bool = True):
         """SUM all-reduce of one wire bucket over the DP group (RCCL), a3 minus the /n."""
         self._replicated_only("all_reduce")
-        before_collective(self.group, self.bucket_view(bucket))
         return dist.all_reduce(self.bucket_view(bucket), op=dist.ReduceOp.SUM, group=self.group,
                                async_op=async_op)
 

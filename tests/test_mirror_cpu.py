@@ -629,3 +629,26 @@ def test_outer_sgd_other_configs_match_plain_torch(placement, momentum, nesterov
             else:
                 assert all(opt.state[p].get("momentum_buffer") is None
                            for p in outer.parameters()), where
+
+
+def test_lazy_host_state_dict_holds_the_last_step():
+    """outer_model.state_dict() of the default host placement (write_back="lazy") after an
+    outer step holds that step's θ with no parameter read first (its detach() goes through
+    HostParameter, which refreshes the host θ arena). Its tensors are plain views of that
+    arena: an alias kept across a later outer step shows the new θ once the arena is refreshed
+    -- by any read through the model or by flush_outer_model."""
+    g = load_npz("micro_n1.npz")
+    inner, outer = _models("lazy")
+    opt = get_optimizer(outer, SGD_CFG)
+    kept = None
+    for s in (1, 2):
+        _set_inner(inner, outer, s)
+        compute_pseudo_gradient(inner, outer)
+        opt.step()
+        sync_inner_model(outer, inner)
+        sd = outer.state_dict()  # nothing read through the parameters before this
+        assert _host(sd.values()).tobytes() == g[f"theta_s{s}"].tobytes(), s
+        if kept is None:
+            kept = sd
+    flush_outer_model(outer)
+    assert _host(kept.values()).tobytes() == g["theta_s2"].tobytes()

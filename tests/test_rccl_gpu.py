@@ -17,7 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import PKG, REPO, load_npz
+from conftest import PKG, REPO, load_npz, spin
 
 pytestmark = pytest.mark.gpu
 
@@ -474,3 +474,101 @@ def test_rccl_single_rank_device_mirror_exchanges():
                 assert rec[f"{ex}_{k}_s{s}"].tobytes() == g[f"{k}_s{s}"].tobytes(), (ex, k, s)
             assert rec[f"{ex}_inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes(), (ex, s)
             assert rec[f"{ex}_avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes(), (ex, s)
+
+
+def _ports():
+    """A port p with p + 1 free too (World puts its TCPStore on MASTER_PORT + 1)."""
+    for _ in range(50):
+        p = _free_port()
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p + 1))
+            except OSError:
+                continue
+        return p
+    raise RuntimeError("no free port pair")
+
+
+def _worker_train_wiring(rank, port, out):
+    """The process groups src/train.py runs with, on one rank: World(swarm)
+    makes the TCPStore and the gloo default group (src/world.py:32-33); TrainingComm over it;
+    the DP group from DPSync.dp_group(cuda) -- the RCCL subgroup created with
+    use_local_synchronization=True (diloco_amd/comm.py). No torch.cuda.set_device: the reference
+    never calls it (src/train.py:368 only names cuda:local_rank). The outer model is built
+    while the inner one is on the CPU (src/train.py:382), both placements; the exchange the
+    mirror makes at n > 1 is called explicitly over the RCCL subgroup (sync_gradients returns
+    early at one peer), its buckets in flight until OuterSGD.step waits on them; a deliberately
+    slow producer (a spin kernel ahead of the packs) on the caller's stream each step."""
+    for p in (PKG, REPO, os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from types import SimpleNamespace
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0", DILOCO_OUTER_BUCKET_ELEMS="4096")
+    from diloco_amd import synth
+    from diloco_amd.comm import TrainingComm
+    from diloco_amd.trees import get_tree
+    from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
+                                  sync_inner_model)
+    from diloco_amd.world import World
+
+    world = World(SimpleNamespace(num_stages=1))
+    rec = {"default_backend": np.array([dist.get_backend()])}
+    comm = TrainingComm(world, (1, 1, 32), None)
+    device = torch.device("cuda", world.local_rank)  # src/utils.py:36-40
+    group = comm.dp.dp_group(device)
+    rec["dp_backend"] = np.array([dist.get_backend(group)])
+    rec["dp_is_default"] = np.array([group is dist.group.WORLD])
+    spec = get_tree("micro")
+    shapes = [s for _, s in spec.params()]
+    theta0 = synth.outer_tree(spec.numels(), spec.init_spec())
+    for placement in ("host", "device"):
+        inner = torch.nn.Module()
+        inner.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.from_numpy(v.copy()).view(s))
+                                           for v, s in zip(theta0, shapes)])
+        outer = get_outer_model(inner, placement)  # src/train.py:382, inner still on the CPU
+        opt = get_optimizer(outer, SimpleNamespace(type="SGD", lr=0.7, momentum=0.9,
+                                                   nesterov=True))
+        inner = inner.to(device)  # src/train.py:163
+        for s in (1, 2):
+            prev = [p.detach().cpu().numpy().reshape(-1).copy() for p in outer.parameters()]
+            with torch.no_grad():
+                for p, v in zip(inner.parameters(), synth.inner_tree(prev, s, 0)):
+                    p.copy_(torch.from_numpy(v).view(p.shape))
+            compute_pseudo_gradient(inner, outer)
+            comm.sync_gradients(outer)  # one peer: returns at once (src/comm.py:118-119)
+            spin(200)  # a slow producer ahead of the packs: dl_spin, 200 ms
+            m = outer._diloco_mirror
+            m.all_reduce(group, 1)  # what sync_gradients makes at n > 1, over the RCCL subgroup
+            dm = getattr(m, "dev", m)
+            rec[f"{placement}_inflight_s{s}"] = np.array([dm._works is not None])
+            opt.step()
+            sync_inner_model(outer, inner)
+            rec[f"{placement}_theta_s{s}"] = _flat(outer.parameters())
+            rec[f"{placement}_buf_s{s}"] = _flat(opt.state[p]["momentum_buffer"]
+                                                 for p in outer.parameters())
+            rec[f"{placement}_inner_s{s}"] = _flat(inner.parameters())
+            rec[f"{placement}_avg_s{s}"] = _flat(p.grad for p in outer.parameters())
+        rec[f"{placement}_device"] = np.array([str(dm.device)])
+        m.close()
+    np.savez(os.path.join(out, "wiring.npz"), **rec)
+    dist.destroy_process_group()
+
+
+def test_train_py_process_groups_rccl_dp_subgroup_over_gloo_default():
+    out = tempfile.mkdtemp(prefix="dl_rccl_wiring_")
+    mp.spawn(_worker_train_wiring, args=(_ports(), out), nprocs=1, join=True)
+    rec = dict(np.load(os.path.join(out, "wiring.npz")))
+    g = load_npz("micro_n1.npz")
+    assert rec["default_backend"][0] == "gloo"
+    assert rec["dp_backend"][0] == "nccl" and not rec["dp_is_default"][0]
+    for placement in ("host", "device"):
+        assert rec[f"{placement}_device"][0] == "cuda:0", placement
+        for s in (1, 2):
+            assert rec[f"{placement}_inflight_s{s}"][0], (placement, s)
+            for k in ("theta", "buf"):
+                assert rec[f"{placement}_{k}_s{s}"].tobytes() == g[f"{k}_s{s}"].tobytes(), \
+                    (placement, k, s)
+            assert rec[f"{placement}_inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+            assert rec[f"{placement}_avg_s{s}"].tobytes() == g[f"delta_s{s}_r0"].tobytes()

@@ -239,3 +239,25 @@ def test_outer_step_called_on_the_engines_own_stream():
     got = np.concatenate([p.reshape(-1).cpu().numpy() for p in params])
     assert got.tobytes() == g["theta_s2"].tobytes()
     e.close()
+
+
+def test_dl_spin_holds_the_stream_for_its_duration():
+    """dl_spin, the slow producer of the ordering tests: a kernel after it on the same stream
+    starts only once the requested time has passed on the device clock (events around it),
+    and the host is not held (the call returns at once)."""
+    import time
+
+    s = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    t = time.perf_counter()
+    _lib.call("dl_spin", 150_000_000, s.cuda_stream)  # 150 ms
+    issued = time.perf_counter() - t
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1)
+    assert 140.0 <= ms <= 400.0, ms
+    assert issued < 0.05
+    with pytest.raises(_lib.DilocoHipError, match="10 s"):
+        _lib.call("dl_spin", 11_000_000_000, s.cuda_stream)

@@ -2,7 +2,7 @@
 """Config #5 through the reference's calls (eight gloo processes on one GPU,
 tests/test_dropin_gpu.py::_bf16_dropin_codec_check) K times per variant: every run's worst
 error / bound and mismatches -- to localise an intermittent missing contribution.
-Variants: base; sync_pack (the current stream synchronized after each bucket's pack, before
+Variants: base (the product: no host wait); sync_pack (the current stream synchronized after each bucket's pack, before
 its all_reduce); sync_wait (synchronized after each bucket's wait, before its SGD pass).
 
     python tools/bf16_n8_repeat.py K variant [variant ...]
@@ -22,22 +22,10 @@ import torch.multiprocessing as mp  # noqa: E402
 
 
 def _patch(variant):
-    from diloco_amd import mirror, staging
+    from diloco_amd import mirror
 
-    if variant in ("nostage", "fence"):
-        # nostage: no wait before a gloo collective (the code before diloco_amd.staging);
-        # fence: no host wait either, but every XCD's L2 written back at system scope on the
-        # caller's stream (dl_sys_fence) ahead of the collective -- if the race is gloo's DMA
-        # copy reading HBM under dirty L2 lines, this alone removes it
-        from diloco_amd.kernels import default_kernels
-
-        k = default_kernels()
-
-        def before(group, t):
-            if variant == "fence" and t.is_cuda and staging.host_staged(group):
-                k.sys_fence(t.device)
-        staging.before_collective = before
-        mirror.before_collective = before
+    if variant == "base":
+        return
     elif variant == "sync_pack":
         orig = mirror.DeviceOuterMirror._launch_reductions
 

@@ -55,6 +55,8 @@ def scan(host, want_bits, m):
 
 
 def worker(proc, nprocs, args, out_q):
+    from diloco_amd import _lib
+
     torch.cuda.set_device(0)
     sizes = bucket_sizes(args.nb)
     dev = [torch.empty(m, dtype=torch.bfloat16, device="cuda") for m in sizes]
@@ -90,7 +92,7 @@ def worker(proc, nprocs, args, out_q):
                 val = float(1 + ((proc * 131 + it * 17 + b) % 120) / 8.0)
                 bits = int(torch.tensor([val], dtype=torch.bfloat16).view(torch.int16).item())
                 if variant == "dep":
-                    torch.cuda._sleep(args.spin)
+                    _lib.call("dl_spin", args.spin_us * 1000, cur.cuda_stream)
                 d.fill_(val)
                 if variant == "nodep":
                     cur.synchronize()
@@ -123,7 +125,7 @@ def main():
     ap.add_argument("--procs", type=int, default=1)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--nb", type=int, default=25)
-    ap.add_argument("--spin", type=int, default=20_000_000)
+    ap.add_argument("--spin-us", type=int, default=10_000)
     ap.add_argument("--variants", default="dep,nodep")
     args = ap.parse_args()
     t0 = time.time()

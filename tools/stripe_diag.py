@@ -55,18 +55,13 @@ def _worker(rank, world, port, out):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    from diloco_amd import mirror, staging, synth
+    from diloco_amd import mirror, synth
     from diloco_amd.comm import TrainingComm
     from diloco_amd.trees import get_tree
     from diloco_amd.utils import (compute_pseudo_gradient, get_optimizer, get_outer_model,
                                   sync_inner_model)
     from diloco_amd.world import World
     from test_dropin_gpu import SGD_CFG
-
-    def no_wait(group, t):
-        return None
-    staging.before_collective = no_wait
-    mirror.before_collective = no_wait
 
     snaps = {}
     orig = mirror.DeviceOuterMirror._launch_reductions
