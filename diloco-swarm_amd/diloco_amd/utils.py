@@ -166,10 +166,13 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
                     exchange: str = None) -> nn.Module:
     """Initializes the outer model from the inner model (src/utils.py:213-216).
 
-    placement "host" (the reference's, default) or "device"; write_back "sync" (default) or
-    "deferred" for the host placement; fused (default on), wire ("f32" default, "bf16":
-    BASELINE config #5's codec on the DP exchange) and exchange ("sharded" default,
-    "replicated", "a2a") for the device placement (see the module docstring)."""
+    placement "host" (the reference's, default) or "device" (in HBM: on the inner model's GPU;
+    built while the inner model is on the CPU, it stays there until the first
+    compute_pseudo_gradient names the device); write_back "lazy" (default: the host outer
+    model stepped on an HBM twin), "sync" or "deferred" for the host placement; fused
+    (default on), wire ("f32" default, "bf16": BASELINE config #5's codec; "int8") and
+    exchange ("sharded" default, "replicated", "a2a") for placement="device" and for the lazy
+    host write-back (see the module docstring)."""
     if placement is None:
         placement = os.environ.get("DILOCO_OUTER_PLACEMENT", "host")
     if placement not in PLACEMENTS:

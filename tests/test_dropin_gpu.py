@@ -101,11 +101,14 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
                            outer.parameters()))
         if spin:
             conftest_spin(spin)
+        t_sync = time.perf_counter()
         if deferred and mid:
             flush_outer_model(outer)
         if mid:
             rec[f"delta_s{s}"] = _flat(p.grad for p in outer.parameters())
         comm.sync_gradients(outer)
+        if spin:  # host time of the call that issued every bucket's collective
+            rec[f"sync_host_ms_s{s}"] = np.float64((time.perf_counter() - t_sync) * 1e3)
         if deferred and mid:
             flush_outer_model(outer)
         if mid:
@@ -229,27 +232,26 @@ def _worker(rank, world, port, mode, out):
                            wire="bf16" if mode == "dropin_device_bf16" else
                            "int8" if "int8" in mode else None)
     elif mode.startswith("slow_producer"):
-        # async ordering behind the reference's calls: no host wait
-        # anywhere, every bucket's collective issued while a spin kernel still holds the packs
-        # back on the caller's stream; bucket b's SGD pass waits for bucket b's Work only.
-        # "_broken": the control -- the packs moved to a side stream the collectives are not
-        # ordered behind (a bug this test must catch)
+        # the reference's calls over two gloo processes with no host wait anywhere, every
+        # bucket's collective issued while a spin kernel still holds the packs back on the
+        # caller's stream; bucket b's SGD pass waits for bucket b's Work only.
+        # "_unordered": the control -- the packs run on a side stream behind the spin, which
+        # the collectives (ordered behind the caller's stream) do not wait for
         os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"
         spin = 200  # ms
-        if mode.endswith("_broken"):
-            from diloco_amd import mirror
+        if mode.endswith("_unordered"):
+            from diloco_amd.kernels import default_kernels
 
-            orig = mirror.DeviceOuterMirror._launch_reductions
-            side = torch.cuda.Stream()
+            k = default_kernels()
+            orig, side, held = k.delta_pack, torch.cuda.Stream(), [False]
 
-            def launch(self, pack, view, group):
-                def pack_on_side(b):
-                    with torch.cuda.stream(side):
-                        if b == 0:
-                            conftest_spin(spin)
-                        pack(b)
-                return orig(self, pack_on_side, view, group)
-            mirror.DeviceOuterMirror._launch_reductions = launch
+            def delta_pack_on_side(*a):
+                with torch.cuda.stream(side):
+                    if not held[0]:
+                        conftest_spin(spin)
+                        held[0] = True
+                    orig(*a)
+            k.delta_pack = delta_pack_on_side
             spin = 0
         rec = _outer_steps(rank, world, placement="host" if "_host" in mode else "device",
                            quiet=True, spin=spin)
@@ -617,9 +619,11 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
     digest = hashlib.sha256()
     faults = []
     for s in range(1, steps + 1):
-        th = [p.detach().view(-1) for p in outer.parameters()]
+        # θ on the device (the default placement's outer parameters are CPU tensors)
+        th = [p.detach().view(-1).to("cuda:0") for p in outer.parameters()]
         inner_tree_device_checked(th, s, rank, [p.data.view(-1) for p in inner.parameters()],
                                   faults)
+        del th
         compute_pseudo_gradient(inner, outer)
         comm.sync_gradients(outer)
         opt.step()
@@ -678,23 +682,27 @@ def test_two_peers_on_gpu_match_reference(mode):
 
 
 @pytest.mark.parametrize("mode", ["slow_producer_device", "slow_producer_host",
-                                  "slow_producer_broken"])
-def test_async_collectives_behind_a_slow_producer(mode):
+                                  "slow_producer_unordered"])
+def test_collectives_behind_a_slow_producer(mode):
     """Two processes, gloo DP group on the device tensors, no host synchronize anywhere: each
-    step's packs queue behind a 200 ms spin kernel (dl_spin) while all bucket collectives are
-    issued at once; the averages must still be the reference's (micro_n2.npz, bit-exact) --
-    gloo's staging copy is ordered behind the packs by the event it records on the caller's
-    stream, and each SGD pass waits on its bucket's Work. The control moves the packs to a side
-    stream the collectives are not ordered behind and must come out wrong: the test sees an
-    ordering bug when there is one."""
+    step's packs queue behind a 200 ms spin kernel (dl_spin) while every bucket's collective
+    (the sharded exchange's reduce_scatter) is issued -- gloo's issuing call returns long
+    before the spin ends, its staging copy ordered behind the caller's stream by an event
+    (tools/gloo_sync_probe.py; `sync_host_ms_s*` records the issue time); the averages must be
+    the reference's (micro_n2.npz, bit-exact), on both placements. The control runs the packs
+    on a side stream the collectives are not ordered behind and must come out wrong: the
+    producer side of the order is really exercised. (gloo's Work.wait() holds the host until
+    the collective is done, where RCCL's only orders the stream: the consumer side is tested
+    against a stream-ordered slow peer in tests/test_async_order_gpu.py.)"""
     recs = _run(mode)
     g = load_npz("micro_n2.npz")
-    ok = all(recs[r][f"theta_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
-             and recs[r][f"buf_s{s}"].tobytes() == g[f"buf_s{s}"].tobytes()
-             and recs[r][f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
-             and recs[r][f"avg_s{s}"].tobytes() == g[f"avg_s{s}"].tobytes()
-             for r in (0, 1) for s in (1, 2))
-    assert ok == (mode != "slow_producer_broken"), mode
+    ok = all(recs[r][f"{k}_s{s}"].tobytes() == g[f"{k}_s{s}"].tobytes()
+             for r in (0, 1) for s in (1, 2) for k in ("theta", "buf", "avg"))
+    ok &= all(recs[r][f"inner_s{s}"].tobytes() == g[f"theta_s{s}"].tobytes()
+              for r in (0, 1) for s in (1, 2))
+    assert ok == (mode != "slow_producer_unordered"), mode
+    if mode != "slow_producer_unordered":  # the calls returned before the producer finished
+        assert all(float(recs[r][f"sync_host_ms_s{s}"]) < 150 for r in (0, 1) for s in (1, 2))
 
 
 def test_t125_two_peers_dropin_device_bit_exact_vs_oracle():
