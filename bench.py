@@ -1408,6 +1408,8 @@ def main():
             return None
         em.running = name
         r = _guard(fn, *args)
+        if ws > 1 and dist.get_backend(dp_group(dev)) == "gloo":
+            torch._C._host_emptyCache()  # gloo's pinned staging blocks of the leg just run
         into[name] = r
         log(f"{name} done at {em.elapsed():.1f} s")
         return r
@@ -1459,8 +1461,13 @@ def main():
                 ks = max(3, a.steps // 4)
                 # get_outer_model's default placement, as the headline: the CPU outer model
                 # holds 4 B/param resident per rank (its θ; the pageable .grad / momentum
-                # arenas fill only when read), 5.3 GB at 1.3B
-                r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1)
+                # arenas fill only when read), 5.3 GB at 1.3B. A gloo rehearsal with
+                # every rank on one GPU keeps these outer models in HBM instead: gloo stages
+                # each rank's whole 1.3B wire and θ through pinned host memory as well (cached
+                # in power-of-two blocks), which eight ranks on one box cannot also hold
+                p13 = "device" if shared_gpu else None
+                r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1, "f32", None,
+                          "sharded", False, False, p13)
                 ref13 = leg(f"rccl_ref_{es.name}", rccl_reference, dev, ws, rank,
                             es.total() // (64 * ws) * (64 * ws), 3, into=em.detail)
                 e = exchange_efficiency(r13, ref13, ws)
@@ -1477,8 +1484,10 @@ def main():
             leg(f"{spec.name}_engine", run_engine, spec, dev, ws, rank, a.steps, a.warmup,
                 torch.float32, cap)
             if es is not None:
-                leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16")
-                leg(f"{es.name}_dropin_int8", run_dropin, es, dev, ws, rank, ks, 1, "int8")
+                leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16", None,
+                    "sharded", False, False, p13)
+                leg(f"{es.name}_dropin_int8", run_dropin, es, dev, ws, rank, ks, 1, "int8", None,
+                    "sharded", False, False, p13)
             leg(f"{spec.name}_grad_sync", gradsync_rate, spec, dev, ws, rank, max(3, a.steps // 2))
             if ws >= 4 and ws % 2 == 0:
                 leg(f"{spec.name}_two_stages", run_two_stages, spec, dev, ws, rank, a.steps,
