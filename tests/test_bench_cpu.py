@@ -192,3 +192,52 @@ def test_dropin_hbm_bytes_per_param():
     assert bench.dropin_bpp(8, "sharded") == 20 + 20 / 8
     assert bench.dropin_bpp(2, "replicated") == 36
     assert bench.dropin_bpp(8, "replicated", "bf16") == 32
+
+
+_WIRING = r"""
+import json, os, sys
+sys.path.insert(0, {repo!r})
+import torch, torch.distributed as dist
+import bench
+from diloco_amd import comm
+comm.DP_BACKEND = "gloo"   # what setup_dist sets under DILOCO_BENCH_BACKEND=gloo
+dist.init_process_group("gloo")   # setup_dist's default group at WORLD_SIZE > 1
+dev = torch.device("cuda", 0)     # only a device object: new_group needs no GPU
+g = bench.dp_group(dev)
+t = torch.tensor([float(dist.get_rank() + 1)])
+dist.all_reduce(t, group=g)
+rec = dict(default=dist.get_backend(), dp=dist.get_backend(g), dp_size=dist.get_world_size(g),
+           distinct=g is not dist.group.WORLD, cached=bench.dp_group(dev) is g,
+           one_comm=bench.training_comm() is bench.training_comm(),
+           cpu_is_stage_group=bench.dp_group(torch.device("cpu"))
+           is bench.training_comm().world.curr_stage_group, sum=t.item())
+if dist.get_rank() == 0:
+    print("REC" + json.dumps(rec), flush=True)
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def test_bench_dp_group_is_train_py_subgroup_over_gloo_default():
+    """bench.py at N > 1 builds src/train.py's process groups: a gloo default group
+    (src/world.py:32-33) and, for device tensors, DPSync's DP subgroup created over it
+    (use_local_synchronization=True); one TrainingComm per run (src/train.py:291). Two CPU
+    processes under torchrun with the DP backend set to gloo, as the one-box rehearsal does."""
+    import socket
+    import tempfile
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    path = os.path.join(tempfile.mkdtemp(prefix="dl_wiring_"), "w.py")
+    with open(path, "w") as f:
+        f.write(_WIRING.format(repo=REPO))
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), path], capture_output=True, text=True, timeout=170, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("REC")][0][3:])
+    assert rec == dict(default="gloo", dp="gloo", dp_size=2, distinct=True, cached=True,
+                       one_comm=True, cpu_is_stage_group=True, sum=3.0), rec
