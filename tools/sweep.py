@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "diloco-swarm_amd"))
 
 import torch  # noqa: E402
 
-from diloco_amd import _lib, synth  # noqa: E402
+from diloco_amd import synth  # noqa: E402
 from diloco_amd.outer import OuterSync  # noqa: E402
 from diloco_amd.trees import get_tree  # noqa: E402
 
