@@ -10,7 +10,9 @@
 //   q8_split   4096-B payload slots (aligned) + a dense fp32 scale array
 //   q8_noscale q8_4160 without the 4-B scale store (payload only)
 //   q8_nobar   q8_4160 with the amax taken per wave (no workgroup barrier; a per-1024 scale)
-//   q8_lds*    the payload staged in LDS, one 16-B store per lane (plain / non-temporal)
+//   q8_lds*    the payload staged in LDS, one 16-B store per lane (plain / non-temporal);
+//              _4224_h128: a 128-B header, so every payload starts on a cache line; plain ld:
+//              default-policy loads instead of non-temporal
 //   packbf_*   the bf16 wire's delta_pack (10 B/elem): 8-B stores per lane vs LDS-staged 16-B
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -fhip-fp32-correctly-rounded-divide-sqrt tools/q8_layout.hip -o build/q8_layout
@@ -41,6 +43,7 @@ constexpr int U = 4;      // float4 per lane per stream
 __device__ __forceinline__ f4 ld(const float* p, long v) {
   return __builtin_nontemporal_load((const G f4*)(p) + v);
 }
+__device__ __forceinline__ f4 ldp(const float* p, long v) { return ((const G f4*)(p))[v]; }
 
 __device__ __forceinline__ float amax4(f4 x) {
   return fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
@@ -110,7 +113,7 @@ __global__ void __launch_bounds__(T) q8enc(const float* th, const float* in, uns
 
 // the payload staged through LDS, then one 16-B store per lane (1 KB per wave instruction
 // instead of four 256-B ones); NTS: non-temporal payload stores
-template <int SLOT, int HDR, bool SPLIT, bool NTS, bool FULLHDR = false>
+template <int SLOT, int HDR, bool SPLIT, bool NTS, bool FULLHDR = false, bool NTL = true>
 __global__ void __launch_bounds__(T) q8lds(const float* th, const float* in, unsigned char* slots,
                                            float* scales) {
   __shared__ unsigned stage[CH / 4];
@@ -119,7 +122,8 @@ __global__ void __launch_bounds__(T) q8lds(const float* th, const float* in, uns
   float am = 0.f;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    d[u] = ld(th, base + u * T + threadIdx.x) - ld(in, base + u * T + threadIdx.x);
+    d[u] = NTL ? ld(th, base + u * T + threadIdx.x) - ld(in, base + u * T + threadIdx.x)
+               : ldp(th, base + u * T + threadIdx.x) - ldp(in, base + u * T + threadIdx.x);
     am = fmaxf(am, amax4(d[u]));
   }
   const float s = chunk_amax<true>(am) / 127.f;
@@ -246,6 +250,9 @@ int main(int argc, char** argv) {
   ADD("q8_lds     4160, 16-B stores ", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, false>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_nt  4160, NT 16-B     ", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, true>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_nt_fullhdr (product) ", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, true, true>), g, b, 0, 0, th, in, slots, scales));
+  ADD("q8_lds_nt_4224_h128 (aligned)", q8b, hipLaunchKernelGGL((q8lds<4224, 128, false, true, true>), g, b, 0, 0, th, in, slots, scales));
+  ADD("q8_lds_nt_fullhdr plain loads", q8b, hipLaunchKernelGGL((q8lds<4160, 64, false, true, true, false>), g, b, 0, 0, th, in, slots, scales));
+  ADD("q8_lds_nt_4224_h128 plain ld ", q8b, hipLaunchKernelGGL((q8lds<4224, 128, false, true, true, false>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_split 4096+scales     ", q8b, hipLaunchKernelGGL((q8lds<4096, 0, true, false>), g, b, 0, 0, th, in, slots, scales));
   ADD("q8_lds_split_nt              ", q8b, hipLaunchKernelGGL((q8lds<4096, 0, true, true>), g, b, 0, 0, th, in, slots, scales));
   unsigned short* wb = reinterpret_cast<unsigned short*>(w);
