@@ -8,10 +8,13 @@
 One step = one outer step of src/train.py:261-269 over the whole synthetic tree on every rank,
 made through the reference's own calls -- compute_pseudo_gradient -> TrainingComm.sync_gradients
 -> outer_optimizer.step() -> sync_inner_model (diloco_amd's drop-in modules, train.py untouched)
--- on the fused device-resident outer model (get_outer_model(..., placement="device")):
+-- on the outer model get_outer_model(inner) returns with its defaults (the reference's CPU
+outer model, stepped on its HBM twin):
     N = 1  one dl_delta_pack_sgd (outer.grad = θ_outer - inner, Nesterov SGD, inner = θ)
-    N > 1  the sharded exchange: per bucket dl_delta_pack -> RCCL reduce_scatter, then per
-           bucket dl_shard_sgd on this rank's 1/n -> RCCL all_gather(θ) -> dl_scatter to inner
+    N > 1  the default placement's replicated exchange (round 6: .grad and the momentum stay
+           local on every rank, as in the reference): per bucket dl_delta_pack -> RCCL
+           all_reduce, then per bucket dl_unpack_sgd (/n, Nesterov SGD, inner = θ); the opt-in
+           sharded form (reduce_scatter -> dl_shard_sgd -> all_gather(θ)) is a side leg
 Same tree per rank at every N (weak scaling). value = 4 * params / t_step ("GB/s
 params reduced": the bytes of ONE parameter tree reduced per DP step, max time over ranks);
 N * 4 * params / t_step is "value_aggregate".
@@ -86,9 +89,8 @@ def setup_dist(n_gpus):
     backend = os.environ.get("DILOCO_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local %= max(1, torch.cuda.device_count())
-        os.environ.setdefault("DILOCO_DP_BACKEND", "gloo")  # the drop-in legs' DP group too
-        if "diloco_amd.comm" in sys.modules:
-            sys.modules["diloco_amd.comm"].DP_BACKEND = os.environ["DILOCO_DP_BACKEND"]
+        # the drop-in legs' DP group too (comm.dp_backend() reads it when the group is made)
+        os.environ.setdefault("DILOCO_DP_BACKEND", "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if ws > 1:
@@ -104,13 +106,21 @@ _COMM: dict = {}
 
 
 def training_comm(n_embd=768):
-    """The run's one TrainingComm (src/train.py:291 makes one), over the default group."""
-    if "comm" not in _COMM:
+    """The run's TrainingComm for activations of width n_embd (src/train.py:291 makes one per
+    run, for its model's shape), over the default group. One per width -- the shape is the
+    pipeline's activation shape -- all sharing the first one's DPSync, so every leg's DP
+    collectives run on the one DP group (one RCCL communicator) of the run."""
+    c = _COMM.get(n_embd)
+    if c is None:
         from diloco_amd.comm import TrainingComm
         from diloco_amd.world import World
 
-        _COMM["comm"] = TrainingComm(World.from_default_group(1), (1, 1, n_embd), None)
-    return _COMM["comm"]
+        c = TrainingComm(World.from_default_group(1), (1, 1, n_embd), None)
+        first = next(iter(_COMM.values()), None)
+        if first is not None:
+            c.dp = first.dp
+        _COMM[n_embd] = c
+    return c
 
 
 def dp_group(dev):
@@ -229,10 +239,11 @@ def _dropin_objects(spec, dev, rank, wire, bucket_elems, exchange, placement=Non
 
 
 def run_dropin(spec, dev, ws, rank, steps, warmup, wire="f32", bucket_elems=None,
-               exchange="sharded", cold=False, synced=False, placement=None):
+               exchange=None, cold=False, synced=False, placement=None):
     """The outer step through the reference's call surface, src/train.py:263-269, on the outer
     model get_outer_model returns (placement None: the default, the reference's CPU outer
-    model stepped on its HBM twin; "device": the outer model in HBM): K steps back to back
+    model stepped on its HBM twin; "device": the outer model in HBM; exchange None: that
+    placement's default, DEFAULT_EXCHANGE): K steps back to back
     between barrier + synchronize (the four Python calls of step k+1 are issued while step k's
     kernels run). synced: a device synchronize after every step, as the reference's loop has
     around its outer step (src/train.py:244), so the calls' host time is exposed; each step is
@@ -858,7 +869,7 @@ def run_two_stages(spec, dev, ws, rank, steps, warmup, cap):
     communicator. value = 2 · 4P / t_step (two trees reduced per step)."""
     from diloco_amd import comm
 
-    groups = [dist.new_group([r for r in range(ws) if r % 2 == s], backend=comm.DP_BACKEND)
+    groups = [dist.new_group([r for r in range(ws) if r % 2 == s], backend=comm.dp_backend())
               for s in range(2)]
     eng = build(spec, dev, rank, torch.float32, cap, group=groups[rank % 2])
     for _ in range(max(warmup, 1)):
@@ -1386,8 +1397,9 @@ def main():
     workload = (f"DiLoCo outer step, {spec.name} tree per rank, through the reference's calls "
                 "(src/train.py:263-269) on get_outer_model's default (CPU) outer model, stepped "
                 "on its HBM twin: "
-                + ("per bucket dl_delta_pack -> RCCL reduce_scatter; dl_shard_sgd on this "
-                   "rank's 1/n -> RCCL all_gather(theta) -> dl_scatter to inner" if ws > 1 else
+                + ("per bucket dl_delta_pack -> RCCL all_reduce (the default placement's "
+                   "replicated exchange: .grad and the momentum local on every rank) -> "
+                   "dl_unpack_sgd (/n, Nesterov SGD, copy to inner)" if ws > 1 else
                    "one dl_delta_pack_sgd per step (delta + outer.grad + Nesterov SGD + copy "
                    "to inner; no exchange at one replica, src/comm.py:118-119)"))
     meta = {"n_gpus": ws, "steps": a.steps, "warmup": a.warmup, "workload": workload}
@@ -1409,7 +1421,11 @@ def main():
         em.running = name
         r = _guard(fn, *args)
         if ws > 1 and dist.get_backend(dp_group(dev)) == "gloo":
-            torch._C._host_emptyCache()  # gloo's pinned staging blocks of the leg just run
+            # gloo's pinned staging blocks of the leg just run (a private torch call: skipped
+            # on a build without it)
+            empty_host_cache = getattr(torch._C, "_host_emptyCache", None)
+            if empty_host_cache is not None:
+                empty_host_cache()
         into[name] = r
         log(f"{name} done at {em.elapsed():.1f} s")
         return r
@@ -1450,9 +1466,9 @@ def main():
                     False)
                 leg(f"{es.name}_int8", run_q8, es, dev, ws, rank, ks, 1, cap)
             leg(f"{spec.name}_dropin_device", run_dropin, spec, dev, ws, rank, a.steps,
-                a.warmup, "f32", None, "sharded", False, False, "device")
+                a.warmup, "f32", None, None, False, False, "device")
             leg(f"{spec.name}_dropin_synced", run_dropin, spec, dev, ws, rank, 30, 1, "f32",
-                None, "sharded", False, True)
+                None, None, False, True)
             leg("dropin_pcie", dropin_pcie, spec, dev, ws, rank, 5)
         else:
             if es is not None:
@@ -1465,9 +1481,11 @@ def main():
                 # every rank on one GPU keeps these outer models in HBM instead: gloo stages
                 # each rank's whole 1.3B wire and θ through pinned host memory as well (cached
                 # in power-of-two blocks), which eight ranks on one box cannot also hold
+                # (with the default placement's exchange, replicated: RCCL's all_reduce itself)
                 p13 = "device" if shared_gpu else None
+                x13 = "replicated" if shared_gpu else None
                 r13 = leg(f"{es.name}_dropin", run_dropin, es, dev, ws, rank, ks, 1, "f32", None,
-                          "sharded", False, False, p13)
+                          x13, False, False, p13)
                 ref13 = leg(f"rccl_ref_{es.name}", rccl_reference, dev, ws, rank,
                             es.total() // (64 * ws) * (64 * ws), 3, into=em.detail)
                 e = exchange_efficiency(r13, ref13, ws)
@@ -1478,16 +1496,16 @@ def main():
             e = exchange_efficiency(head, ref, ws)
             if e:
                 exch[spec.name] = e
-            for ex in ("replicated", "a2a"):
+            for ex in ("sharded", "a2a"):  # the opt-in exchanges (the headline is replicated)
                 leg(f"{spec.name}_dropin_{ex}", run_dropin, spec, dev, ws, rank, a.steps,
                     a.warmup, "f32", None, ex)
             leg(f"{spec.name}_engine", run_engine, spec, dev, ws, rank, a.steps, a.warmup,
                 torch.float32, cap)
             if es is not None:
                 leg(f"{es.name}_dropin_bf16", run_dropin, es, dev, ws, rank, ks, 1, "bf16", None,
-                    "sharded", False, False, p13)
+                    x13, False, False, p13)
                 leg(f"{es.name}_dropin_int8", run_dropin, es, dev, ws, rank, ks, 1, "int8", None,
-                    "sharded", False, False, p13)
+                    x13, False, False, p13)
             leg(f"{spec.name}_grad_sync", gradsync_rate, spec, dev, ws, rank, max(3, a.steps // 2))
             if ws >= 4 and ws % 2 == 0:
                 leg(f"{spec.name}_two_stages", run_two_stages, spec, dev, ws, rank, a.steps,

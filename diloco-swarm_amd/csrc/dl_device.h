@@ -60,6 +60,18 @@ constexpr int kAuxSc1 = 16;  // buffer-op cache policy bits, gfx950: sc0 = 1, nt
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7fffffff, 0x00020000);
 }
+// Store-order A/B of dl_delta_pack_sgd (tools/store_order_ab.py builds the variants; the
+// product build uses the defaults): DL_DPS_ORDER picks the order of its four output streams,
+// DL_DPS_WIRE_PLAIN stores the wire with plain stores while θ, momentum and inner follow the
+// launch's store policy.
+#ifndef DL_DPS_ORDER
+#define DL_DPS_ORDER 0
+#endif
+#ifdef DL_DPS_WIRE_PLAIN
+#define DL_DPS_WIRE_NTS(n) kStPlain
+#else
+#define DL_DPS_WIRE_NTS(n) (n)
+#endif
 template <int SP>
 __device__ __forceinline__ void stf4(float* p, int v, float4 x) {
   const f32x4 r = {x.x, x.y, x.z, x.w};
@@ -153,12 +165,26 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 // DL_TUNE_AUTO selects: non-temporal loads with plain or non-temporal stores. `make TUNING=1`
 // (-DDL_TUNING) instantiates the whole matrix -- plain loads, write-through for every body --
 // for the measurement tools (tools/cold_sweep.py); dl_tree_tune rejects the rest otherwise.
+// Workgroup -> chunk. The dispatcher hands workgroup b to XCD b mod 8, so by default the
+// eight XCDs walk the range interleaved chunk by chunk. DL_XCD_CONTIG (A/B build,
+// tools/store_order_ab.py): with one workgroup per chunk, XCD x takes the x-th eighth of the
+// range instead, in order (n = 8q + r: XCDs below r take q + 1 chunks).
+__device__ __forceinline__ int32_t walk_index(int32_t b, int32_t n) {
+#ifdef DL_XCD_CONTIG
+  if (int32_t(gridDim.x) == n) {
+    const int32_t q = n >> 3, r = n & 7, x = b & 7, k = b >> 3;
+    return x * q + (x < r ? x : r) + k;
+  }
+#endif
+  return b;
+}
+
 template <class Body, bool NTL, int NTS>
 __global__ void __launch_bounds__(kThreads)
     k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ caddr,
            int32_t nchunk, Body body) {
-  for (int32_t i = int32_t(blockIdx.x); i < c1 - c0; i += int32_t(gridDim.x)) {
-    const int32_t c = c0 + i;
+  for (int32_t i0 = int32_t(blockIdx.x); i0 < c1 - c0; i0 += int32_t(gridDim.x)) {
+    const int32_t c = c0 + walk_index(i0, c1 - c0);
     const Chunk ck = chunks[c];
     body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x));
   }

@@ -312,8 +312,20 @@ struct DeltaPackSgd {
         }
       }
 #pragma unroll
+      for (int u = 0; u < kUnroll; ++u) x[u] = sub4(t[u], x[u]);  // the pseudo-gradient
+      // Store order of the four output streams (DL_DPS_ORDER, tools/store_order_ab.py; the
+      // product build is 0): 0 = the SGD arithmetic, then wire, θ, momentum, inner, each
+      // stream's rows back to back; 1 = the wire rows issued before the SGD arithmetic;
+      // 2 = row by row across the four streams; 3 = inner, momentum, θ, wire.
+#if DL_DPS_ORDER == 1
+#pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        x[u] = sub4(t[u], x[u]);  // the pseudo-gradient, kept for the wire stores
+        const int v = u * kThreads + tid;
+        if (v < nv) WireIO<W>::template st4<DL_DPS_WIRE_NTS(NTS)>(w, v, x[u]);
+      }
+#endif
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
         const float4 g = make_float4(on_wire(x[u].x), on_wire(x[u].y), on_wire(x[u].z),
                                      on_wire(x[u].w));
         sgd1<MODE>(g.x, m[u].x, t[u].x, a);
@@ -321,14 +333,38 @@ struct DeltaPackSgd {
         sgd1<MODE>(g.z, m[u].z, t[u].z, a);
         sgd1<MODE>(g.w, m[u].w, t[u].w, a);
       }
+#if DL_DPS_ORDER == 2
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int v = u * kThreads + tid;
-        if (v < nv) WireIO<W>::template st4<NTS>(w, v, x[u]);
+        if (v < nv) {
+          WireIO<W>::template st4<DL_DPS_WIRE_NTS(NTS)>(w, v, x[u]);
+          stf4<NTS>(th, v, t[u]);
+          if (MODE != 0) stf4<NTS>(mb, v, m[u]);
+          stf4<NTS>(in, v, t[u]);
+        }
       }
+#elif DL_DPS_ORDER == 3
+      store_rows<NTS>(in, t, nv, tid);
+      if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
+      store_rows<NTS>(th, t, nv, tid);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int v = u * kThreads + tid;
+        if (v < nv) WireIO<W>::template st4<DL_DPS_WIRE_NTS(NTS)>(w, v, x[u]);
+      }
+#else
+#if DL_DPS_ORDER == 0
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int v = u * kThreads + tid;
+        if (v < nv) WireIO<W>::template st4<DL_DPS_WIRE_NTS(NTS)>(w, v, x[u]);
+      }
+#endif
       store_rows<NTS>(th, t, nv, tid);
       if (MODE != 0) store_rows<NTS>(mb, m, nv, tid);
       store_rows<NTS>(in, t, nv, tid);
+#endif
       const int i = (nv << 2) + tid;
       if (i < ck.len) {
         const float g0 = th[i] - in[i];
@@ -978,8 +1014,10 @@ __global__ void __launch_bounds__(64) k_spin(uint64_t ticks) {
 }
 
 hipError_t launch_spin(uint64_t ns, hipStream_t s) {
-  int dev = 0, khz = 0;
-  hipError_t e = hipGetDevice(&dev);
+  // the wall-clock rate of the device the stream launches on (not the caller's current one)
+  hipDevice_t dev = 0;
+  int khz = 0;
+  hipError_t e = hipStreamGetDevice(s, &dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
   if (e != hipSuccess) return e;
   const uint64_t ticks = ns * uint64_t(khz > 0 ? khz : 100000) / 1000000ull;

@@ -141,7 +141,13 @@ class RecvThread:
 # Collective backend of the DP group for device tensors: "nccl" = RCCL over xGMI (the
 # product). "gloo" exists for multi-process tests that share one GPU (RCCL refuses two ranks
 # on one device); the kernels are the same HIP kernels either way.
-DP_BACKEND = os.environ.get("DILOCO_DP_BACKEND", "nccl")
+# None: DILOCO_DP_BACKEND as it is when the group is created ("nccl" if unset), like
+# p2p.p2p_backend(); a value assigned here overrides it.
+DP_BACKEND: Optional[str] = None
+
+
+def dp_backend() -> str:
+    return DP_BACKEND or os.environ.get("DILOCO_DP_BACKEND", "nccl")
 # The DP average's exchange: "rccl" = RCCL's own order (the device-gradient GradSync's
 # all_reduce; the outer model's exchange as get_outer_model chose it); "a2a" = all_to_all +
 # rank-order average + all_gather (deterministic, bit-exact vs the oracle at any n) for the
@@ -171,7 +177,7 @@ class DPSync:
             return self.world.curr_stage_group
         if self._rccl_group is None:
             self._rccl_group = dist.new_group(self.world.stage2ranks[self.world.stage],
-                                              backend=DP_BACKEND, use_local_synchronization=True)
+                                              backend=dp_backend(), use_local_synchronization=True)
         return self._rccl_group
 
     def sync_gradients(self, model: nn.Module) -> None:

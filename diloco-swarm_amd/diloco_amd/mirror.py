@@ -64,10 +64,68 @@ OUTER_WIRES = ("f32", "bf16", "int8")
 #   "replicated"  per bucket RCCL all_reduce -> the SGD pass on the whole tree on every rank
 #   "a2a"         "sharded" with an all_to_all + rank-order sum (bit-exact at every n)
 OUTER_EXCHANGES = ("sharded", "replicated", "a2a")
+# get_outer_model's default per placement (round 6): the reference's
+# outer.grad and momentum buffers are local CPU tensors (src/utils.py:218-221, torch SGD state
+# at src/train.py:267), so the host placement defaults to "replicated" -- every rank holds the
+# whole average and momentum after each step, every read is local, at the same bus bytes as the
+# sharded form (an all_reduce is a reduce_scatter + all_gather) and a full SGD pass per rank.
+# The device placement keeps "sharded": its reads of .grad / the momentum at N > 1 are
+# collectives, guarded by collective_read() so that a one-rank read raises instead of hanging.
+DEFAULT_EXCHANGE = {"host": "replicated", "device": "sharded"}
 
 
 def _none():
     return None
+
+
+_READ_SEQ: dict = {}
+
+
+def collective_read(group, what: str) -> None:
+    """Entry of a read that is a collective over the DP group (under the sharded exchange a
+    rank holds 1/n of the averaged .grad and of the momentum; reading either gathers the rest
+    from its peers). Before the all_gathers start, the ranks agree through the job's
+    rendezvous store that every one of them is making this read: the k-th read of `what` on
+    this group counts its arrivals, and the last arrival sets the read's state to "go"; a rank
+    still waiting after DILOCO_COLLECTIVE_READ_TIMEOUT seconds (default 30) sets it to "abort".
+    compare_set makes the two outcomes exclusive, so a read either runs on every rank or raises
+    RuntimeError on every rank that enters it -- also a peer arriving after the deadline --
+    instead of leaving one rank blocked in an all_gather its peers never make."""
+    import os
+    from datetime import timedelta
+
+    if group is None:
+        group = dist.group.WORLD
+    n = dist.get_world_size(group)
+    if n <= 1:
+        return
+    from torch.distributed import distributed_c10d as c10d
+
+    get_store = getattr(c10d, "_get_default_store", None)
+    if get_store is None:
+        raise RuntimeError("torch.distributed has no rendezvous store to agree on a collective "
+                           "read; use exchange='replicated' (every read local)")
+    store = get_store()
+    ranks = tuple(dist.get_process_group_ranks(group))
+    seq = _READ_SEQ.get((ranks, what), 0) + 1
+    _READ_SEQ[(ranks, what)] = seq
+    key = f"diloco/collective_read/{what}/{','.join(map(str, ranks))}/{seq}"
+    timeout = float(os.environ.get("DILOCO_COLLECTIVE_READ_TIMEOUT", "30"))
+    if store.add(key + "/arrived", 1) >= n:
+        state = store.compare_set(key + "/state", "", "go")
+    else:
+        try:
+            store.wait([key + "/state"], timedelta(seconds=timeout))
+        except Exception:  # the deadline passed: decided below, atomically
+            pass
+        state = store.compare_set(key + "/state", "", "abort")
+    if bytes(state) != b"go":
+        raise RuntimeError(
+            f"reading the outer model's {what} at N > 1 under the sharded exchange is a "
+            f"collective over the DP group (ranks {list(ranks)}), and not every rank made this "
+            f"read within {timeout:g} s (DILOCO_COLLECTIVE_READ_TIMEOUT). Read it on every "
+            "rank, call flush_outer_model(outer_model) on every rank first, or use "
+            "exchange='replicated' (the host placement's default: every read local)")
 
 
 def ordered_average(k, tree, wire: torch.Tensor, recv: torch.Tensor, group, n: int,
@@ -794,6 +852,7 @@ class DeviceOuterMirror:
     def _gather_wire(self) -> None:
         """The pending sharded wire -> every bucket's full Σ (or average) on every rank: the
         a2a slices reduced in rank order, then an in-place all_gather per bucket."""
+        collective_read(self._xgroup, "grad")
         mode, self._xmode = self._xmode, None
         n, r, g = self._xn, self._xrank, self._xgroup
         for b in range(self.tree.n_buckets):
@@ -808,8 +867,9 @@ class DeviceOuterMirror:
         slices): an in-place all_gather per bucket over the DP group of those steps."""
         if not self._mom_stale:
             return
-        self._mom_stale = False
         g, n, r = self._mom_shard
+        collective_read(g, "momentum")
+        self._mom_stale = False
         for b in range(self.tree.n_buckets):
             lo, hi = self.tree.bucket_ranges[b]
             a, e = self._own(b, n, r)
@@ -1449,19 +1509,20 @@ class LazyHostOuterMirror:
     The outer model's parameters stay the CPU Parameters the reference returns, their .grad
     and the optimizer's momentum buffers CPU tensors -- views of three pinned host arenas
     (θ, grad, momentum) laid out like the device's. The outer step itself runs on an HBM twin
-    of the outer model (a DeviceOuterMirror: the fused one-pass kernel at one peer, the sharded
-    RCCL exchange at N > 1, no PCIe traffic per step). A host arena is copied from HBM (one
+    of the outer model (a DeviceOuterMirror: the fused one-pass kernel at one peer, the RCCL
+    exchange at N > 1 -- replicated by default, so .grad and the momentum stay local on every
+    rank -- no PCIe traffic per step). A host arena is copied from HBM (one
     DMA) only when something reads one of its tensors after the device changed it
     (HostParameter / HostTensor intercept every read), and host-side writes are uploaded before
     the next outer-step call (detected by the arenas' version counters and by assignments of
     `.data` / `.grad`). So every value a caller observes is the reference's, on the CPU,
-    while an outer step that nobody observes costs what the device placement costs. Reading
-    `.grad` or the momentum under the sharded exchange at N > 1 is a collective over the DP
-    group, as for the device placement."""
+    while an outer step that nobody observes costs what the device placement costs. Under an
+    opted-in sharded exchange at N > 1, reading `.grad` or the momentum is a collective over
+    the DP group, as for the device placement (collective_read guards it)."""
 
     def __init__(self, outer_model: torch.nn.Module, device: torch.device, kernels=None,
                  bucket_cap_elems: int = DEFAULT_BUCKET_CAP_ELEMS, fused: bool = True,
-                 wire: str = "f32", exchange: str = "sharded"):
+                 wire: str = "f32", exchange: str = DEFAULT_EXCHANGE["host"]):
         self.device = torch.device(device)
         params = module_params(outer_model)
         if not params:

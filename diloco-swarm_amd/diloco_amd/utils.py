@@ -37,12 +37,15 @@ For "device" and "host"/"lazy": fused (`get_outer_model(..., fused=)`, DILOCO_OU
 if unset) runs the four calls as one HBM pass at one peer (dl_delta_pack_sgd) and as
 pack -> exchange -> one SGD pass at N > 1, with .grad completing the deferred work when read
 and sync_inner_model a verified no-op after the step; wire (DILOCO_OUTER_WIRE, "f32";
-"bf16": BASELINE config #5's codec on the DP exchange); exchange (DILOCO_OUTER_EXCHANGE,
-"sharded": reduce_scatter -> SGD on this rank's 1/n -> all_gather of θ, SURVEY §8e;
-"replicated": all_reduce -> the SGD pass on every rank; "a2a": the sharded form with a
-rank-order sum, bit-exact at every n; DILOCO_DP_EXCHANGE=a2a selects it too). Under the
-sharded forms a read of .grad or of the momentum buffers at N > 1 gathers them from the peers:
-a collective over the DP group, made by every rank.
+"bf16": BASELINE config #5's codec on the DP exchange); exchange (DILOCO_OUTER_EXCHANGE;
+"replicated", the host placement's default: all_reduce -> the SGD pass on every rank, so
+.grad and the momentum are local on every rank as in the reference; "sharded", the device
+placement's default: reduce_scatter -> SGD on this rank's 1/n -> all_gather of θ, SURVEY §8e;
+"a2a": the sharded form with a rank-order sum, bit-exact at every n; DILOCO_DP_EXCHANGE=a2a
+selects it too). Under the sharded forms a read of .grad or of the momentum buffers at N > 1
+gathers them from the peers: a collective over the DP group that every rank must make; a read
+its peers do not make raises RuntimeError after DILOCO_COLLECTIVE_READ_TIMEOUT seconds
+(mirror.collective_read) instead of hanging.
 """
 from __future__ import annotations
 
@@ -54,8 +57,8 @@ import torch.nn as nn
 from torch.optim import SGD, AdamW, Optimizer
 
 from .kernels import default_kernels
-from .mirror import (OUTER_EXCHANGES, OUTER_WIRES, WRITE_BACKS, DeviceOuterMirror,
-                     HostOuterMirror, LazyHostOuterMirror, module_params)
+from .mirror import (DEFAULT_EXCHANGE, OUTER_EXCHANGES, OUTER_WIRES, WRITE_BACKS,
+                     DeviceOuterMirror, HostOuterMirror, LazyHostOuterMirror, module_params)
 from .optim import OuterSGD
 from .plan import DEFAULT_BUCKET_CAP_ELEMS
 
@@ -120,7 +123,8 @@ def outer_mirror(outer_model: nn.Module, device=None):
             m = DeviceOuterMirror(outer_model, dev, kernels=k, bucket_cap_elems=cap,
                                   fused=getattr(outer_model, _FUSED, False),
                                   wire=getattr(outer_model, _WIRE, "f32"),
-                                  exchange=getattr(outer_model, _EXCHANGE, "sharded"),
+                                  exchange=getattr(outer_model, _EXCHANGE,
+                                                   DEFAULT_EXCHANGE["device"]),
                                   keep_params=keep)
             object.__setattr__(outer_model, _ATTR, m)
             return m
@@ -137,7 +141,8 @@ def outer_mirror(outer_model: nn.Module, device=None):
                                     bucket_cap_elems=cap,
                                     fused=getattr(outer_model, _FUSED, True),
                                     wire=getattr(outer_model, _WIRE, "f32"),
-                                    exchange=getattr(outer_model, _EXCHANGE, "sharded"))
+                                    exchange=getattr(outer_model, _EXCHANGE,
+                                                     DEFAULT_EXCHANGE["host"]))
         else:
             m = HostOuterMirror(outer_model, torch.device(device), kernels=k, write_back=wb)
         object.__setattr__(outer_model, _ATTR, m)  # not a submodule / not in state_dict
@@ -171,8 +176,9 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     compute_pseudo_gradient names the device); write_back "lazy" (default: the host outer
     model stepped on an HBM twin), "sync" or "deferred" for the host placement; fused
     (default on), wire ("f32" default, "bf16": BASELINE config #5's codec; "int8") and
-    exchange ("sharded" default, "replicated", "a2a") for placement="device" and for the lazy
-    host write-back (see the module docstring)."""
+    exchange ("replicated" for the host placement and "sharded" for placement="device" by
+    default, or "a2a") for placement="device" and for the lazy host write-back (see the module
+    docstring)."""
     if placement is None:
         placement = os.environ.get("DILOCO_OUTER_PLACEMENT", "host")
     if placement not in PLACEMENTS:
@@ -188,7 +194,7 @@ def get_outer_model(inner_model: nn.Module, placement: str = None,
     if wire not in OUTER_WIRES:
         raise ValueError(f"wire {wire!r}: one of {OUTER_WIRES}")
     if exchange is None:
-        exchange = os.environ.get("DILOCO_OUTER_EXCHANGE", "sharded")
+        exchange = os.environ.get("DILOCO_OUTER_EXCHANGE") or DEFAULT_EXCHANGE[placement]
     if exchange not in OUTER_EXCHANGES:
         raise ValueError(f"exchange {exchange!r}: one of {OUTER_EXCHANGES}")
     lazy = placement == "device" or write_back == "lazy"  # the outer step runs on an HBM copy

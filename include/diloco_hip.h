@@ -254,8 +254,10 @@ DL_API int dl_serialize_f64(const double* src, int64_t numel, float meta0, float
  * all fp32 ops correctly rounded: bit-identical to diloco_amd.synth (numpy). */
 DL_API int dl_fill_synth(float* dst, int64_t n, uint64_t seed, uint64_t stream_id, float base,
                          float scale, const float* add, dl_stream_t stream);
-/* A slow producer for ordering tests: one workgroup that occupies `stream` for `ns`
- * nanoseconds of the device's wall clock (at most 10 s), touching no memory. */
+/* TEST SUPPORT, not part of the outer step: a slow producer for the ordering tests
+ * (tests/test_async_order_gpu.py, the slow-producer cases of tests/test_dropin_gpu.py): one
+ * workgroup that occupies `stream` for `ns` nanoseconds of the wall clock of the device
+ * `stream` belongs to (at most 10 s), touching no memory. */
 DL_API int dl_spin(uint64_t ns, dl_stream_t stream);
 
 /* ---- RCCL ------------------------------------------------------------

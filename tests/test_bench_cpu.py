@@ -168,8 +168,33 @@ def test_line_is_compact_with_every_leg_present(ws):
     assert all(set(v) == {"ok", "err"} for v in d["parity"].values())
     if ws > 1:
         assert d["exchange_efficiency"]["t1.3b"]["rccl_allreduce_busbw_GBs"] == 300.0
+        # the N > 1 line carries the parity the driver's SCALE run needs
+        for k in ("f32", "dropin_exchanges"):
+            assert d["parity"][k]["ok"] is True and d["parity"][k]["err"] < 1e-6, k
     # nothing had to be dropped for these records
     assert "legs_dropped_from_line" not in d
+
+
+def test_committed_n8_rehearsal_line_carries_parity_and_exchange_efficiency():
+    """The newest committed N = 8 rehearsal line (bench.py with eight ranks at its default
+    deadline, profiles/r*_bench_n8_gloo_rehearsal.json) carries parity.f32,
+    parity.dropin_exchanges (both ok) and exchange_efficiency -- the figures the driver's
+    SCALE run reads -- within the 4 KB line bound."""
+    import glob as _glob
+    import sys as _sys
+
+    _sys.path.insert(0, REPO)
+    import bench
+
+    paths = sorted(_glob.glob(os.path.join(REPO, "profiles", "r*_bench_n8_gloo_rehearsal.json")))
+    assert paths
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    assert d["n_gpus"] == 8 and d["dtype"] == "f32"
+    for k in ("f32", "dropin_exchanges"):
+        assert d["parity"][k]["ok"] is True, k
+    assert "t1.3b" in d["exchange_efficiency"]
+    assert len(json.dumps(d)) <= bench.LINE_MAX_BYTES
 
 
 def test_line_drops_side_legs_rather_than_grow():

@@ -77,8 +77,8 @@ def _worker(rank, world, port, mode, num_stages, out):
                 "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
                 "dropin_device_a2a_dp", "dropin_a2a_dp", "dropin_device_momentum_first",
                 "dropin_device_eager_a2a_dp", "dropin_sync", "dropin_sync_a2a_dp",
-                "dropin_quiet", "dropin_device_int8", "dropin_device_int8_eager",
-                "dropin_int8"):
+                "dropin_quiet", "dropin_quiet_sharded", "dropin_device_int8",
+                "dropin_device_int8_eager", "dropin_int8"):
         if mode in ("dropin_device_quiet_buckets", "dropin_device_quiet_a2a",
                     "dropin_device_momentum_first", "dropin_device_int8",
                     "dropin_device_int8_eager", "dropin_int8"):  # several buckets: the
@@ -88,6 +88,7 @@ def _worker(rank, world, port, mode, num_stages, out):
 
             comm_mod.DP_EXCHANGE = "a2a"
         exchange = ("replicated" if mode.endswith("_replicated")
+                    else "sharded" if mode.endswith("_sharded")
                     else "a2a" if mode == "dropin_device_quiet_a2a" else None)
         from diloco_amd.utils import flush_outer_model, has_mirror
 
@@ -100,7 +101,7 @@ def _worker(rank, world, port, mode, num_stages, out):
         quiet = mode in ("dropin_device_quiet", "dropin_device_bf16", "dropin_device_quiet_buckets",
                          "dropin_device_quiet_replicated", "dropin_device_quiet_a2a",
                          "dropin_device_a2a_dp", "dropin_device_momentum_first", "dropin_quiet",
-                         "dropin_device_int8")
+                         "dropin_quiet_sharded", "dropin_device_int8")
         device = mode.startswith("dropin_device")
         inner = _micro_module(theta0, shapes)
         outer = get_outer_model(inner, placement="device" if device else None,
@@ -372,6 +373,62 @@ def _worker(rank, world, port, mode, num_stages, out):
             rec[f"ref_avg_s{s}"] = host(p.grad for p in ref_outer.parameters())
             rec[f"ref_exp_avg_sq_s{s}"] = host(ref_opt.state[p]["exp_avg_sq"]
                                                for p in ref_outer.parameters())
+    elif mode in ("lone_read_default", "lone_read_sharded", "lone_read_device"):
+        # after an outer step, rank 0 alone reads the outer optimizer's
+        # state_dict() and .grad -- in the reference local CPU tensors (src/utils.py:218-221,
+        # torch SGD state at src/train.py:267). Default placement (replicated exchange): the
+        # reference's values, and the peers go on to the next step. Sharded (opted in on the
+        # host placement; the device placement's default): the read is a collective its peer
+        # does not make -> RuntimeError within the deadline, and the peer's late read of the
+        # same values raises too instead of entering an all_gather alone.
+        import time
+
+        os.environ["DILOCO_COLLECTIVE_READ_TIMEOUT"] = "3"
+        sharded = mode != "lone_read_default"
+        inner = _micro_module(theta0, shapes)
+        outer = get_outer_model(inner, placement="device" if mode == "lone_read_device" else None,
+                                exchange="sharded" if mode == "lone_read_sharded" else None)
+        from diloco_amd.utils import outer_mirror
+
+        m = outer_mirror(outer)
+        rec["exchange"] = np.array(getattr(m, "dev", m).exchange)
+        opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
+        comm = TrainingComm(world_, (1, 1, 32), None)
+
+        def host(ts):
+            return np.concatenate([t.detach().numpy().reshape(-1) for t in ts])
+
+        def outer_step(s):  # src/train.py:263-269, nothing read in between
+            vals = synth.inner_tree([p.detach().numpy().reshape(-1).copy()
+                                     for p in outer.parameters()], s, dp_rank)
+            with torch.no_grad():
+                for p, v in zip(inner.parameters(), vals):
+                    p.copy_(torch.from_numpy(v).view(p.shape))
+            compute_pseudo_gradient(inner, outer)
+            comm.sync_gradients(outer)
+            opt.step()
+            sync_inner_model(outer, inner)
+
+        outer_step(1)
+        reads = (("state_dict", lambda: host(st["momentum_buffer"]
+                                            for st in opt.state_dict()["state"].values())),
+                 ("grad", lambda: host(p.grad for p in outer.parameters())))
+        if dp_rank == 0 or sharded:
+            if dp_rank != 0:
+                time.sleep(7.0)  # past rank 0's two deadlines: the same reads, late
+            for name, read in reads:
+                t0 = time.time()
+                try:
+                    rec[f"{name}_s1"] = read()
+                    rec[f"{name}_outcome"] = np.array("values")
+                except RuntimeError as e:
+                    rec[f"{name}_outcome"] = np.array("raised")
+                    rec[f"{name}_msg"] = np.array(str(e))
+                rec[f"{name}_secs"] = np.float64(time.time() - t0)
+        if not sharded:  # the group is intact: a second step, read on every rank
+            outer_step(2)
+            rec["theta_s2"] = host(outer.parameters())
+            rec["grad_s2"] = host(p.grad for p in outer.parameters())
     elif mode == "outputs":
         comm = TrainingComm(world_, (1, 1, 4), None)
         o = Outputs(step=3, tokens=100 * (rank + 1), num_micro_batches=rank, time=1.0 + rank,
@@ -397,6 +454,7 @@ def _run(mode, world, num_stages=1):
                                   "dropin_device_quiet_a2a", "dropin_device_a2a_dp",
                                   "dropin_a2a_dp", "dropin_device_momentum_first",
                                   "dropin_device_eager_a2a_dp", "dropin_sync", "dropin_quiet",
+                                  "dropin_quiet_sharded",
                                   "dropin_sync_a2a_dp",
                                   "dropin_device_eager", "dropin_deferred", "engine",
                                   "engine_ar", "engine_a2a", "dropin_host"])
@@ -413,8 +471,10 @@ def test_two_peers_match_reference_bit_exact(mode):
     if mode.startswith("dropin") and "delta_s1" in recs[0]:
         assert recs[0]["delta_s1"].tobytes() == g["delta_s1_r0"].tobytes()
         assert recs[1]["delta_s1"].tobytes() == g["delta_s1_rlast"].tobytes()
-    if "sharded_step" in recs[0]:  # the fused device model's exchange: sharded unless asked
-        want = not mode.endswith("_replicated")
+    if "sharded_step" in recs[0]:  # which exchange ran: the device placement's default is
+        # sharded, the host placement's replicated (reads local)
+        want = ((mode.startswith("dropin_device") and not mode.endswith("_replicated"))
+                or mode.endswith("_sharded"))
         assert all(bool(r["sharded_step"].all()) == want for r in recs), mode
 
 
@@ -442,7 +502,8 @@ def test_dropin_ordered_exchange_is_bit_exact_at_any_n(mode, world):
                                         ("dropin_device_quiet_buckets", 4),
                                         ("dropin_device_quiet_buckets", 8),
                                         ("dropin_device_momentum_first", 8),
-                                        ("dropin_quiet", 8), ("dropin_sync", 4),
+                                        ("dropin_quiet", 8), ("dropin_quiet_sharded", 8),
+                                        ("dropin_sync", 4),
                                         ("dropin_device_quiet_replicated", 4)])
 def test_four_and_eight_peers_match_reference_normwise(mode, world):
     """4 and 8 DP peers (8: the north star's DP = 8) against the reference's own gloo run."""
@@ -458,6 +519,40 @@ def test_four_and_eight_peers_match_reference_normwise(mode, world):
                     assert normwise_ok(a, b, 1e-6), (mode, k, s)
     for s in (1, 2):  # every replica holds the same averaged state
         assert all(r[f"theta_s{s}"].tobytes() == recs[0][f"theta_s{s}"].tobytes() for r in recs)
+
+
+def test_lone_read_on_the_default_placement_is_local():
+    """on get_outer_model's default placement rank 0 alone reads the outer
+    optimizer's state_dict() and .grad after an outer step; both are the reference's values
+    (micro_n2.npz: the momentum and the average after step 1), and the two ranks then make
+    a second step that is still the reference's."""
+    g = load_npz("micro_n2.npz")
+    r0, r1 = _run("lone_read_default", 2)
+    assert str(r0["exchange"]) == "replicated"
+    assert str(r0["state_dict_outcome"]) == "values" and str(r0["grad_outcome"]) == "values"
+    assert r0["state_dict_s1"].tobytes() == g["buf_s1"].tobytes()
+    assert r0["grad_s1"].tobytes() == g["avg_s1"].tobytes()
+    assert "state_dict_outcome" not in r1  # rank 1 read nothing
+    for r in (r0, r1):
+        assert r["theta_s2"].tobytes() == g["theta_s2"].tobytes()
+        assert r["grad_s2"].tobytes() == g["avg_s2"].tobytes()
+
+
+@pytest.mark.parametrize("mode", ["lone_read_sharded", "lone_read_device"])
+def test_lone_collective_read_raises_within_the_deadline(mode):
+    """Under the sharded exchange (opted in on the host placement; the device placement's
+    default) the same lone read is a collective its peer does not make: it raises
+    RuntimeError on rank 0 within the 3 s deadline (DILOCO_COLLECTIVE_READ_TIMEOUT) instead of
+    hanging, and rank 1's later reads of the same values raise at once instead of entering an
+    all_gather alone."""
+    r0, r1 = _run(mode, 2)
+    assert str(r0["exchange"]) == "sharded"
+    for name in ("state_dict", "grad"):
+        assert str(r0[f"{name}_outcome"]) == "raised", name
+        assert "collective over the DP group" in str(r0[f"{name}_msg"])
+        assert 2.5 <= float(r0[f"{name}_secs"]) < 8.0, float(r0[f"{name}_secs"])
+        assert str(r1[f"{name}_outcome"]) == "raised", name
+        assert float(r1[f"{name}_secs"]) < 2.0, float(r1[f"{name}_secs"])
 
 
 def test_sharded_engine_checkpoint_resume_two_peers():

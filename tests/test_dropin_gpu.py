@@ -19,8 +19,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import PKG, REPO, inner_tree_device_checked, load_json, load_npz
+from conftest import PKG, REPO, inner_tree_device_verified, load_json, load_npz
 from conftest import spin as conftest_spin
+from gpu_platform import gpu_state as _gpu_state
 
 pytestmark = pytest.mark.gpu
 
@@ -469,9 +470,9 @@ def _adamw_outer_steps(rank, world, device, steps=3):
 def _pack_probe(m, picks):
     """Snapshots of the packed wire over the sampled tensors, taken right after each bucket's
     pack on the same stream: this rank's own delta as it entered the exchange. Compared with
-    the exact delta after the step, a mismatch there is work the shared platform lost (its
-    inputs are checked, the pack is bit-exact in every single-process test), not
-    an exchange result."""
+    the exact delta after the step, a mismatch localises a failure to the pack (inputs
+    verified before it) rather than the exchange; it fails the test like any other (DESIGN
+    §5)."""
     snaps = {}
     k = m.k
     orig = k.delta_pack
@@ -496,21 +497,6 @@ def _lost_pack(snaps, t, own, bf16):
     got = snaps[t].float().cpu().numpy() if bf16 else snaps[t].cpu().numpy()
     want = oracle.bf16_round(own) if bf16 else own
     return int(np.count_nonzero(got.view(np.int32) != np.asarray(want, np.float32).view(np.int32)))
-
-
-def _run_platform_checked(mode, world):
-    """_run, once more if a rank's failure coincides with a lost pack on some rank (the
-    platform fault of DESIGN §5, reported as a warning); a failure without one stands."""
-    recs = _run(mode, world)
-    failed = any(list(r["bad"]) != ["none"] for r in recs)
-    lost = [(r, rec["lost_pack"].tolist()) for r, rec in enumerate(recs)
-            if int(rec["lost_pack"][0][0]) >= 0]
-    if failed and lost:
-        import warnings
-
-        warnings.warn(f"{mode}: a pack lost stores on the shared GPU {lost[:4]}; run again")
-        recs = _run(mode, world)
-    return recs
 
 
 def _bf16_dropin_codec_check(rank, world, steps=2, tree="t1.3b"):
@@ -548,7 +534,7 @@ def _bf16_dropin_codec_check(rank, world, steps=2, tree="t1.3b"):
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     snaps = _pack_probe(outer._diloco_mirror, picks)
     bad, worst, digest = [], 0.0, hashlib.sha256()
-    faults, lost = [], []
+    lost = []
     ops, ips = list(outer.parameters()), list(inner.parameters())
 
     def window(x, t, lo, m):
@@ -559,7 +545,7 @@ def _bf16_dropin_codec_check(rank, world, steps=2, tree="t1.3b"):
                             None if s == 1 else window(opt.state[ops[t]]["momentum_buffer"], t, lo, m))
                   for t, lo, m in picks}
         th = [p.detach().view(-1) for p in ops]
-        inner_tree_device_checked(th, s, rank, [p.data.view(-1) for p in ips], faults)
+        inner_tree_device_verified(th, s, rank, [p.data.view(-1) for p in ips])
         compute_pseudo_gradient(inner, outer)
         comm.sync_gradients(outer)
         opt.step()
@@ -602,8 +588,7 @@ def _bf16_dropin_codec_check(rank, world, steps=2, tree="t1.3b"):
             digest.update(g.tobytes())
     return {"bad": np.array(bad or ["none"]), "checked": np.int64(len(picks) * steps),
             "worst": np.float64(worst), "digest": np.array(digest.hexdigest()),
-            "input_faults": np.array(faults or [(-1, -1, 0)]),
-            "lost_pack": np.array(lost or [(-1, -1, 0)])}
+            "lost_pack": np.array(lost or [(-1, -1, 0)]), "gpu": np.array(repr(_gpu_state()))}
 
 
 def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
@@ -671,12 +656,10 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
     snaps = _pack_probe(dm, picks)
     bad, lost = [], []
     digest = hashlib.sha256()
-    faults = []
     for s in range(1, steps + 1):
         # θ on the device (the default placement's outer parameters are CPU tensors)
         th = [p.detach().view(-1).to("cuda:0") for p in outer.parameters()]
-        inner_tree_device_checked(th, s, rank, [p.data.view(-1) for p in inner.parameters()],
-                                  faults)
+        inner_tree_device_verified(th, s, rank, [p.data.view(-1) for p in inner.parameters()])
         del th
         compute_pseudo_gradient(inner, outer)
         comm.sync_gradients(outer)
@@ -703,22 +686,24 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
                     bad.append(f"step {s} tensor {t} {k}")
     return {"bad": np.array(bad or ["none"]), "checked": np.int64(len(picks) * steps),
             "digest": np.array(digest.hexdigest()),
-            "input_faults": np.array(faults or [(-1, -1, 0)]),
-            "lost_pack": np.array(lost or [(-1, -1, 0)])}
+            "lost_pack": np.array(lost or [(-1, -1, 0)]), "gpu": np.array(repr(_gpu_state()))}
 
 
 def _run(mode, world=2):  # noqa: D401
     out = tempfile.mkdtemp(prefix="dl_gpu_")
     mp.spawn(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True)
-    recs = [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
-    for r, rec in enumerate(recs):  # input fills the shared platform lost (conftest)
-        f = rec.get("input_faults")
-        if f is not None and int(f[0][0]) >= 0:
-            import warnings
+    return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
-            warnings.warn(f"{mode} rank {r}: input generation regenerated after a lost fill "
-                          f"(tensor, attempt, elements): {f.tolist()[:4]}")
-    return recs
+
+def _check_eight_peers(recs):
+    """Config #4 / #5 with eight processes: every rank's checks clean, its own packed delta
+    exact (a lost pack is a failure, not a retry), all replicas bit-identical."""
+    info = [f"rank {r}: GPU state {str(rec.get('gpu', ''))}" for r, rec in enumerate(recs)]
+    for r, rec in enumerate(recs):
+        assert rec["checked"] == 22
+        assert int(rec["lost_pack"][0][0]) < 0, (r, rec["lost_pack"].tolist(), info)
+        assert list(rec["bad"]) == ["none"], (r, list(rec["bad"])[:10], info)
+    assert len({str(rec["digest"]) for rec in recs}) == 1
 
 
 @pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_device_quiet",
@@ -821,11 +806,7 @@ def test_t13b_eight_peers_dropin_device_vs_oracle():
     of HBM each): θ, momentum, inner and .grad within 1e-6 normwise of the C oracle's
     rank-order result on a wte window, block 0 and the last tensor after each of 2 outer
     steps, and all eight replicas bit-identical."""
-    recs = _run_platform_checked("dropin_device_t13b_n8", 8)
-    for rec in recs:
-        assert rec["checked"] == 22
-        assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
-    assert len({str(rec["digest"]) for rec in recs}) == 1
+    _check_eight_peers(_run("dropin_device_t13b_n8", 8))
 
 
 def test_t13b_eight_peers_dropin_device_bf16_wire_within_codec_bound():
@@ -833,11 +814,8 @@ def test_t13b_eight_peers_dropin_device_bf16_wire_within_codec_bound():
     the reference's four calls with eight processes on the one GPU: .grad within the codec's
     a-priori bound of the fp32 average, θ / momentum / inner exactly torch's SGD-Nesterov of
     that .grad, replicas bit-identical (see _bf16_dropin_codec_check)."""
-    recs = _run_platform_checked("dropin_device_t13b_bf16_n8", 8)
-    for rec in recs:
-        assert rec["checked"] == 22
-        assert list(rec["bad"]) == ["none"], list(rec["bad"])[:10]
-    assert len({str(rec["digest"]) for rec in recs}) == 1
+    recs = _run("dropin_device_t13b_bf16_n8", 8)
+    _check_eight_peers(recs)
     print(f"bf16 wire, 8 peers: worst codec error / bound {float(recs[0]['worst']):.3f}")
 
 

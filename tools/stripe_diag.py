@@ -26,7 +26,8 @@ import tempfile
 import time
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(HERE, "tests"), HERE, os.path.join(HERE, "diloco-swarm_amd")):
+for p in (os.path.join(HERE, "tests"), HERE, os.path.join(HERE, "diloco-swarm_amd"),
+          os.path.join(HERE, "tools")):
     sys.path.insert(0, p)
 
 import numpy as np  # noqa: E402
@@ -91,7 +92,19 @@ def _worker(rank, world, port, out):
     opt = get_optimizer(outer, SGD_CFG)
     comm = TrainingComm(World.from_default_group(1), (1, 1, spec.n_embd), None)
     ops, ips = list(outer.parameters()), list(inner.parameters())
-    rec = {}
+    from queue_oversub_probe import kfd_queues, our_gpu_ids, own_evicted_ms
+
+    gids = set(our_gpu_ids())
+
+    def gpu_state():
+        """free HBM (GiB), the GPU's KFD processes / compute queues, their eviction ms"""
+        q = kfd_queues()
+        ours = [v for v in q.values() if any(k[6:] in gids for k in v["evicted_ms"])]
+        return {"free_gb": round(torch.cuda.mem_get_info()[0] / 2**30, 1),
+                "procs": len(ours), "cq": sum(v["queues"].get("0", 0) for v in ours),
+                "evicted_ms": own_evicted_ms()}
+
+    rec = {"gpu": [gpu_state()]}
     for s in (1, 2):
         snaps.clear()
         th = [p.detach().view(-1) for p in ops]
@@ -103,6 +116,7 @@ def _worker(rank, world, port, out):
         opt.step()
         sync_inner_model(outer, inner)
         torch.cuda.synchronize()
+        rec["gpu"].append(gpu_state())
         for t, lo, m in WIN:
             theta = snaps[("theta", t)].cpu().numpy()
             u = synth.uniform(synth.noise_seed(s, rank), t, m, start=lo)
@@ -120,6 +134,8 @@ def _worker(rank, world, port, out):
                                                           & (want_inner != theta)))}
             if any(r[k] for k in ("pack", "inner_q", "inner_h")):
                 rec[f"s{s}_t{t}"] = r
+    if len(rec) == 1 and rank != 0:
+        rec = {}
     np.save(os.path.join(out, f"r{rank}.npy"), np.array([repr(rec)]))
     dist.barrier()
     dist.destroy_process_group()
@@ -136,8 +152,9 @@ if __name__ == "__main__":
         out = tempfile.mkdtemp()
         mp.spawn(_worker, args=(8, t._free_port(), out), nprocs=8, join=True)
         recs = {r: str(np.load(os.path.join(out, f"r{r}.npy"))[0]) for r in range(8)}
-        bad = {r: v for r, v in recs.items() if v != "{}"}
-        print(i, f"{time.time() - t0:.0f}s", bad if bad else "clean", flush=True)
+        bad = {r: v for r, v in recs.items() if v != "{}" and (r != 0 or "'s" in v)}
+        print(i, f"{time.time() - t0:.0f}s", "rank0", recs[0][:400], bad if bad else "clean",
+              flush=True)
         fails += bool(bad)
         if fails >= max_fails:
             break
