@@ -169,11 +169,21 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 // eight XCDs walk the range interleaved chunk by chunk. DL_XCD_CONTIG (A/B build,
 // tools/store_order_ab.py): with one workgroup per chunk, XCD x takes the x-th eighth of the
 // range instead, in order (n = 8q + r: XCDs below r take q + 1 chunks).
+// DL_XCD_BLOCK=B (A/B build): XCD x takes runs of B consecutive chunks -- its k-th
+// workgroup the chunk ((k / B) * 8 + x) * B + k % B -- over the whole super-blocks of 8B
+// chunks, the tail as by default (a bijection on [0, n)).
 __device__ __forceinline__ int32_t walk_index(int32_t b, int32_t n) {
 #ifdef DL_XCD_CONTIG
   if (int32_t(gridDim.x) == n) {
     const int32_t q = n >> 3, r = n & 7, x = b & 7, k = b >> 3;
     return x * q + (x < r ? x : r) + k;
+  }
+#elif defined(DL_XCD_BLOCK)
+  constexpr int32_t B = DL_XCD_BLOCK;
+  const int32_t full = n / (8 * B) * (8 * B);
+  if (int32_t(gridDim.x) == n && b < full) {
+    const int32_t x = b & 7, k = b >> 3;
+    return ((k / B) * 8 + x) * B + k % B;
   }
 #endif
   return b;

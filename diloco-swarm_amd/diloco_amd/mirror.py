@@ -78,9 +78,6 @@ def _none():
     return None
 
 
-_READ_SEQ: dict = {}
-
-
 def collective_read(group, what: str) -> None:
     """Entry of a read that is a collective over the DP group (under the sharded exchange a
     rank holds 1/n of the averaged .grad and of the momentum; reading either gathers the rest
@@ -106,10 +103,12 @@ def collective_read(group, what: str) -> None:
         raise RuntimeError("torch.distributed has no rendezvous store to agree on a collective "
                            "read; use exchange='replicated' (every read local)")
     store = get_store()
-    ranks = tuple(dist.get_process_group_ranks(group))
-    seq = _READ_SEQ.get((ranks, what), 0) + 1
-    _READ_SEQ[(ranks, what)] = seq
-    key = f"diloco/collective_read/{what}/{','.join(map(str, ranks))}/{seq}"
+    ranks = ",".join(map(str, dist.get_process_group_ranks(group)))
+    base = f"diloco/collective_read/{what}/{ranks}"
+    # this rank's count of such reads, kept in the store itself: a new process group (a new
+    # store) starts every rank at 1 again
+    seq = store.add(f"{base}/seq/{dist.get_rank()}", 1)
+    key = f"{base}/{seq}"
     timeout = float(os.environ.get("DILOCO_COLLECTIVE_READ_TIMEOUT", "30"))
     if store.add(key + "/arrived", 1) >= n:
         state = store.compare_set(key + "/state", "", "go")
@@ -122,7 +121,7 @@ def collective_read(group, what: str) -> None:
     if bytes(state) != b"go":
         raise RuntimeError(
             f"reading the outer model's {what} at N > 1 under the sharded exchange is a "
-            f"collective over the DP group (ranks {list(ranks)}), and not every rank made this "
+            f"collective over the DP group (ranks [{ranks}]), and not every rank made this "
             f"read within {timeout:g} s (DILOCO_COLLECTIVE_READ_TIMEOUT). Read it on every "
             "rank, call flush_outer_model(outer_model) on every rank first, or use "
             "exchange='replicated' (the host placement's default: every read local)")

@@ -40,16 +40,18 @@ def cp_queue_slots():
 
 
 def gpu_state():
-    """{free_gb, procs, compute_queues, sdma_queues, evicted_ms} for this box's GPU."""
+    """{free_gb, procs (with the GPU open), procs_with_queues (in the scheduler's runlist),
+    compute_queues, sdma_queues, evicted_ms, cp_queue_slots} for this box's GPU."""
     import torch
 
     gids = set(our_gpu_ids())
-    procs = cq = sq = ev = 0
+    procs = with_queues = cq = sq = ev = 0
     for d in glob.glob("/sys/class/kfd/kfd/proc/*"):
         mine = [g for g in gids if os.path.isdir(os.path.join(d, f"stats_{g}"))]
         if not mine:
             continue
         procs += 1
+        with_queues += bool(glob.glob(os.path.join(d, "queues", "*")))
         for g in mine:
             try:
                 ev += int(_read(os.path.join(d, f"stats_{g}", "evicted_ms")) or 0)
@@ -60,5 +62,6 @@ def gpu_state():
             cq += t == "0"
             sq += t in ("1", "4")
     free = torch.cuda.mem_get_info()[0] / 2**30 if torch.cuda.is_available() else 0.0
-    return {"free_gb": round(free, 1), "procs": procs, "compute_queues": cq, "sdma_queues": sq,
+    return {"free_gb": round(free, 1), "procs": procs, "procs_with_queues": with_queues,
+            "compute_queues": cq, "sdma_queues": sq,
             "evicted_ms": ev, "cp_queue_slots": cp_queue_slots()}

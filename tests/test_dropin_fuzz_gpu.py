@@ -104,7 +104,8 @@ def _run_case(case, rank, world, dev):
     inner.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.from_numpy(t.copy()).view(s))
                                        for t, s in zip(c["theta0"], shapes)])
     wire = "int8" if c["exchange"] == "int8" else None
-    exchange = None if c["exchange"] in ("sharded", "int8") else c["exchange"]
+    # every exchange by name: the placements' defaults differ (host replicated, device sharded)
+    exchange = None if c["exchange"] == "int8" else c["exchange"]
     outer = get_outer_model(inner, c["placement"], wire=wire, exchange=exchange)
     inner = inner.to(dev)
     opt = get_optimizer(outer, _Cfg(type="SGD", lr=c["lr"], momentum=momentum,

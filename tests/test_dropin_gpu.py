@@ -52,7 +52,7 @@ def _flat(ts):
 
 
 def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=None,
-                 write_back=None, quiet=False, fused=None, wire=None, spin=0):
+                 write_back=None, quiet=False, fused=None, wire=None, spin=0, exchange=None):
     """The reference's outer step sequence with the drop-in functions (this process = DP
     rank `rank` of `n`; the default process group must exist). quiet: nothing is read between
     the four calls (src/train.py:261-269 reads nothing), so a fused device outer model defers
@@ -71,7 +71,8 @@ def _outer_steps(rank, n, steps=2, stock_sgd=False, host_shift=0.0, placement=No
     shapes = [s for _, s in spec.params()]
     inner = _module(synth.outer_tree(spec.numels(), spec.init_spec()), shapes, "cpu")
     # src/train.py:382: before the inner model moves
-    outer = get_outer_model(inner, placement, write_back=write_back, fused=fused, wire=wire)
+    outer = get_outer_model(inner, placement, write_back=write_back, fused=fused, wire=wire,
+                            exchange=exchange)
     deferred = write_back == "deferred"
     inner = inner.to("cuda:0")
     if placement == "device":
@@ -220,8 +221,9 @@ def _worker(rank, world, port, mode, out):
     rec = {}
     if mode in ("dropin", "dropin_device", "dropin_deferred", "dropin_device_quiet",
                 "dropin_device_bf16", "dropin_device_quiet_buckets", "dropin_quiet_buckets",
-                "dropin_sync", "dropin_device_int8", "dropin_int8"):
-        if mode.endswith("_quiet_buckets") or "int8" in mode:  # several buckets: bucket b's
+                "dropin_sync", "dropin_device_int8", "dropin_int8",
+                "dropin_quiet_buckets_sharded"):
+        if "_quiet_buckets" in mode or "int8" in mode:  # several buckets: bucket b's
             os.environ["DILOCO_OUTER_BUCKET_ELEMS"] = "4096"  # waits for b's collective only
         rec = _outer_steps(rank, world,
                            placement="device" if mode.startswith("dropin_device") else None,
@@ -229,7 +231,8 @@ def _worker(rank, world, port, mode, out):
                            "sync" if mode == "dropin_sync" else None,
                            quiet=mode in ("dropin_device_quiet", "dropin_device_bf16",
                                           "dropin_device_quiet_buckets", "dropin_quiet_buckets",
-                                          "dropin_device_int8"),
+                                          "dropin_device_int8", "dropin_quiet_buckets_sharded"),
+                           exchange="sharded" if mode.endswith("_sharded") else None,
                            wire="bf16" if mode == "dropin_device_bf16" else
                            "int8" if "int8" in mode else None)
     elif mode.startswith("slow_producer"):
@@ -405,7 +408,7 @@ def _worker(rank, world, port, mode, out):
 
 def _adamw_outer_steps(rank, world, device, steps=3):
     """An AdamW outer optimizer (src/utils.py:60-61) through the four calls with the HIP
-    kernels, the sharded exchange in several buckets; beside it, in this process, the
+    kernels in several buckets (each placement's default exchange); beside it, in this process, the
     reference's calls on a plain deepcopy outer model with per-tensor all_reduce / n -- on the
     CPU as the reference places it, or in HBM beside the device placement (torch's AdamW
     rounds differently on the GPU, and that optimizer is torch's in both)."""
@@ -689,9 +692,27 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
             "lost_pack": np.array(lost or [(-1, -1, 0)]), "gpu": np.array(repr(_gpu_state()))}
 
 
+# Hardware queues per rank process when eight ranks share the one GPU: each process's queues
+# (torch's streams up to GPU_MAX_HW_QUEUES, gloo's high-priority copy stream, one more) enter
+# the firmware scheduler's runlist, which has num_cp_queues = 24 slots. At the default 4 the
+# eight ranks hold 48 and the scheduler time-slices them, remapping processes to new VMIDs
+# mid-step; at 1 they hold 24 and no remap happens (profiles/r06_platform_probes.txt
+# I / J). One process per GPU, the product's shape, holds at most 6.
+EIGHT_PEER_HW_QUEUES = "1"
+
+
 def _run(mode, world=2):  # noqa: D401
     out = tempfile.mkdtemp(prefix="dl_gpu_")
-    mp.spawn(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True)
+    prev = os.environ.get("GPU_MAX_HW_QUEUES")
+    if world > 2:  # the spawned ranks read it at their HIP initialisation
+        os.environ["GPU_MAX_HW_QUEUES"] = EIGHT_PEER_HW_QUEUES
+    try:
+        mp.spawn(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True)
+    finally:
+        if prev is None:
+            os.environ.pop("GPU_MAX_HW_QUEUES", None)
+        else:
+            os.environ["GPU_MAX_HW_QUEUES"] = prev
     return [dict(np.load(os.path.join(out, f"{mode}_r{r}.npz"))) for r in range(world)]
 
 
@@ -708,12 +729,14 @@ def _check_eight_peers(recs):
 
 @pytest.mark.parametrize("mode", ["dropin", "dropin_device", "dropin_device_quiet",
                                   "dropin_device_quiet_buckets", "dropin_quiet_buckets",
-                                  "dropin_sync", "dropin_deferred", "engine", "engine_ar"])
+                                  "dropin_quiet_buckets_sharded", "dropin_sync", "dropin_deferred",
+                                  "engine", "engine_ar"])
 def test_two_peers_on_gpu_match_reference(mode):
     """Two processes on the GPU, gloo DP group: dropin / dropin_quiet_buckets = the default
-    placement (the CPU outer model on its HBM twin; the sharded exchange, several buckets in
-    flight), dropin_sync / dropin_deferred = host-authoritative write-backs, dropin_device* =
-    the outer model in HBM; every value bit-exact vs the reference's 2-peer run."""
+    placement (the CPU outer model on its HBM twin; its replicated exchange, several buckets in
+    flight; _sharded: the opt-in sharded exchange on it), dropin_sync / dropin_deferred =
+    host-authoritative write-backs, dropin_device* = the outer model in HBM (sharded by
+    default); every value bit-exact vs the reference's 2-peer run."""
     g = load_npz("micro_n2.npz")
     for rec in _run(mode):
         for s in (1, 2):
@@ -729,7 +752,8 @@ def test_two_peers_on_gpu_match_reference(mode):
 def test_collectives_behind_a_slow_producer(mode):
     """Two processes, gloo DP group on the device tensors, no host synchronize anywhere: each
     step's packs queue behind a 200 ms spin kernel (dl_spin) while every bucket's collective
-    (the sharded exchange's reduce_scatter) is issued -- gloo's issuing call returns long
+    (the device placement's reduce_scatter, the host placement's all_reduce) is issued --
+    gloo's issuing call returns long
     before the spin ends, its staging copy ordered behind the caller's stream by an event
     (tools/gloo_sync_probe.py; `sync_host_ms_s*` records the issue time); the averages must be
     the reference's (micro_n2.npz, bit-exact), on both placements. The control runs the packs
@@ -762,8 +786,8 @@ def test_t125_two_peers_dropin_device_bit_exact_vs_oracle():
 
 def test_t125_two_peers_dropin_default_placement_bit_exact_vs_oracle():
     """BASELINE config #3 on the outer model src/train.py gets: get_outer_model(inner) with
-    its defaults (the CPU outer model, stepped on its HBM twin, sharded exchange over the gloo
-    DP group); θ, .grad and the momentum read as CPU tensors, and the inner params, bit-exact
+    its defaults (the CPU outer model, stepped on its HBM twin, its replicated exchange over
+    the gloo DP group); θ, .grad and the momentum read as CPU tensors, and the inner params, bit-exact
     against the C oracle on the whole wte, block 0 and the last tensor after each of 2 steps."""
     recs = _run("dropin_host_t125")
     for r in recs:
@@ -1125,8 +1149,9 @@ def test_dropin_int8_wire_two_peers_on_gpu(mode):
 @pytest.mark.parametrize("mode", ["adamw_lazy", "adamw_device"])
 def test_dropin_adamw_outer_optimizer_two_peers_on_gpu(mode):
     """An AdamW outer optimizer (src/utils.py:60-61) on the default lazy host and the device
-    outer model with the HIP kernels: two processes, the sharded exchange in several buckets,
-    AdamW reading the gathered .grad and writing θ in place; three outer steps byte-equal to
+    outer model with the HIP kernels: two processes, several buckets (the host placement's
+    replicated exchange, the device placement's sharded one: AdamW reading the gathered .grad),
+    AdamW writing θ in place; three outer steps byte-equal to
     the reference's calls on a plain deepcopy outer model (per-tensor all_reduce / n) on the
     same device as the outer model's parameters."""
     recs = _run(mode)

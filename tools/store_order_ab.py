@@ -16,6 +16,7 @@ kernels are launched on:
   reverse     inner, momentum, θ, then the wire
   wire_plain  the wire stored plainly, θ / momentum / inner non-temporally
   xcd_contig  XCD x walks the x-th eighth of the chunk range in order (not interleaved)
+  xcd_b<B>    XCD x walks runs of B consecutive chunks (B = 1 is the default interleave)
 
     python tools/store_order_ab.py --build                  # here (hipcc, no GPU)
     python tools/store_order_ab.py --tree t1.3b --rounds 6  # on the GPU box
@@ -38,7 +39,10 @@ FLAGS = ("--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fvisibility=hidden
 SRCS = ["dl_kernels.hip", "dl_q8.hip", "dl_xgmi.hip", "dl_comm.hip", "dl_abi.hip"]
 VARIANTS = {"base": [], "wire_first": ["-DDL_DPS_ORDER=1"], "rows": ["-DDL_DPS_ORDER=2"],
             "reverse": ["-DDL_DPS_ORDER=3"], "wire_plain": ["-DDL_DPS_WIRE_PLAIN"],
-            "xcd_contig": ["-DDL_XCD_CONTIG"]}
+            "xcd_contig": ["-DDL_XCD_CONTIG"], "xcd_b4": ["-DDL_XCD_BLOCK=4"],
+            "xcd_b8": ["-DDL_XCD_BLOCK=8"], "xcd_b16": ["-DDL_XCD_BLOCK=16"], "xcd_b32": ["-DDL_XCD_BLOCK=32"],
+            "xcd_b64": ["-DDL_XCD_BLOCK=64"], "xcd_b256": ["-DDL_XCD_BLOCK=256"],
+            "xcd_b2048": ["-DDL_XCD_BLOCK=2048"]}
 DL_TUNE_NT_LOADS = 1
 
 
@@ -62,6 +66,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default=None, help="comma-separated variants (plain: the base "
+                    "library with plain stores)")
     a = ap.parse_args()
     if a.build:
         build()
@@ -80,7 +86,8 @@ def main():
     libs, trees = {}, {}
     i64 = ctypes.c_int64
     arr = (i64 * len(numels))(*numels)
-    for name in VARIANTS:
+    for name in ([n for n in VARIANTS if n in set(a.only.split(",")) | {"base"}]
+                 if a.only else VARIANTS):
         lib = ctypes.CDLL(os.path.join(OUT, f"lib_{name}.so"), mode=ctypes.RTLD_LOCAL)
         for fn, args in _lib.SIGNATURES.items():
             f = getattr(lib, fn)
@@ -99,9 +106,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream
     ptrs = (ctypes.c_uint64 * len(inner))(*[x.data_ptr() for x in inner])
-    for name in VARIANTS:
+    for name in libs:
         assert libs[name].dl_tree_bind(trees[name], 0, ptrs, len(inner), s) == 0
     runs = [(n, n, None) for n in VARIANTS] + [("plain", "base", DL_TUNE_NT_LOADS)]
+    if a.only:
+        keep = set(a.only.split(",")) | {"base"}
+        runs = [r for r in runs if r[0] in keep]
 
     def launch(lib, tree):
         rc = lib.dl_delta_pack_sgd(tree, -1, 0, theta.data_ptr(), wire.data_ptr(), 0,

@@ -105,14 +105,64 @@ def _worker(rank, world, port, out):
                 "evicted_ms": own_evicted_ms()}
 
     rec = {"gpu": [gpu_state()]}
+    census = os.environ.get("STRIPE_CENSUS") == "1"
+    if census:  # the wte fill through tools/fill_census.hip: every workgroup leaves records
+        import ctypes
+
+        fc = ctypes.CDLL(os.path.join(HERE, "build_ab", "libfill_census.so"))
+        fc.fc_fill.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64,
+                               ctypes.c_float, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_void_p]
+        n0 = ips[0].numel()
+        marks = torch.zeros(2, (n0 + 255) // 256, dtype=torch.int32, device="cuda")
     for s in (1, 2):
         snaps.clear()
         th = [p.detach().view(-1) for p in ops]
-        synth.inner_tree_device(th, s, rank, out=[p.data.view(-1) for p in ips])
+        if census:
+            marks.zero_()
+            seed = synth.noise_seed(s, rank)
+            st = torch.cuda.current_stream().cuda_stream
+            for t, (x, y) in enumerate(zip(th, [p.data.view(-1) for p in ips])):
+                if t == 0:
+                    assert fc.fc_fill(y.data_ptr(), y.numel(), seed, 0, 0.0, synth.NOISE_SCALE,
+                                      x.data_ptr(), marks[0].data_ptr(), marks[1].data_ptr(),
+                                      st) == 0
+                else:
+                    synth.fill_device(y, seed, t, 0.0, synth.NOISE_SCALE, add=x)
+        else:
+            synth.inner_tree_device(th, s, rank, out=[p.data.view(-1) for p in ips])
         compute_pseudo_gradient(inner, outer)
         comm.sync_gradients(outer)
         torch.cuda.synchronize()
         inner_h = {t: ips[t].detach().view(-1)[lo:lo + m].cpu().numpy() for t, lo, m in WIN}
+        if census:  # the whole wte against a second generation, with the workgroups' records
+            ref = torch.empty_like(ips[0].detach().view(-1))
+            synth.fill_device(ref, synth.noise_seed(s, rank), 0, 0.0, synth.NOISE_SCALE,
+                              add=th[0])
+            y = ips[0].detach().view(-1)
+            nb = marks.shape[1]
+            pad = torch.zeros(nb * 256, dtype=torch.bool, device="cuda")
+            pad[:y.numel()] = ref != y
+            badb = pad.view(nb, 256).any(1)
+            m0, m1 = marks[0].cpu().numpy().astype(np.uint32), marks[1].cpu().numpy().astype(np.uint32)
+            badb = badb.cpu().numpy()
+            xcc = (m0 >> 24) & 0xF
+            bidx = np.arange(nb)
+            c = {"blocks": int(nb), "bad_blocks": int(badb.sum()),
+                 "no_start": int((m0 == 0).sum()), "no_end": int((m1 == 0).sum()),
+                 "xcc_ne_block_mod8": int(((m0 != 0) & (xcc != bidx % 8)).sum()),
+                 "vmids": sorted(set(((m0[m0 != 0] >> 16) & 0xF).tolist()))}
+            if badb.any():
+                bb = np.flatnonzero(badb)
+                c["bad_phase"] = np.bincount(bb % 8, minlength=8).tolist()
+                c["bad_start_end"] = {f"{int(a)}{int(b)}": int(((m0[bb] != 0) == a)
+                                                              .__and__((m1[bb] != 0) == b).sum())
+                                      for a in (0, 1) for b in (0, 1)}
+                c["bad_xcc"] = np.bincount(xcc[bb], minlength=8).tolist()
+                c["bad_first_last"] = [int(bb[0]), int(bb[-1])]
+                c["bad_is_theta"] = int((y == th[0]).logical_and(ref != th[0]).sum())
+            rec[f"census_s{s}"] = c
+            del ref, pad
         opt.step()
         sync_inner_model(outer, inner)
         torch.cuda.synchronize()
@@ -134,7 +184,8 @@ def _worker(rank, world, port, out):
                                                           & (want_inner != theta)))}
             if any(r[k] for k in ("pack", "inner_q", "inner_h")):
                 rec[f"s{s}_t{t}"] = r
-    if len(rec) == 1 and rank != 0:
+    if rank != 0 and not any(k.startswith("s") or (k.startswith("census") and v["bad_blocks"])
+                             for k, v in rec.items()):
         rec = {}
     np.save(os.path.join(out, f"r{rank}.npy"), np.array([repr(rec)]))
     dist.barrier()
@@ -152,8 +203,9 @@ if __name__ == "__main__":
         out = tempfile.mkdtemp()
         mp.spawn(_worker, args=(8, t._free_port(), out), nprocs=8, join=True)
         recs = {r: str(np.load(os.path.join(out, f"r{r}.npy"))[0]) for r in range(8)}
-        bad = {r: v for r, v in recs.items() if v != "{}" and (r != 0 or "'s" in v)}
-        print(i, f"{time.time() - t0:.0f}s", "rank0", recs[0][:400], bad if bad else "clean",
+        bad = {r: v for r, v in recs.items()
+               if "'s1_t" in v or "'s2_t" in v or "bad_phase" in v}
+        print(i, f"{time.time() - t0:.0f}s", "rank0", recs[0][:900], bad if bad else "clean",
               flush=True)
         fails += bool(bad)
         if fails >= max_fails:
