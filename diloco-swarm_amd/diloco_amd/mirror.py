@@ -634,7 +634,10 @@ class DeviceOuterMirror:
                  wire: str = "f32", exchange: str = "sharded", keep_params: bool = False):
         """keep_params: the outer model's Parameter objects stay the ones it has (their class
         switched to OuterParameter in place) -- for an outer model that got its device only
-        at its first compute_pseudo_gradient, after get_optimizer took references to them."""
+        at its first compute_pseudo_gradient, after get_optimizer took references to them.
+        Its parameters may then still be the CPU tensors the model was built with: each is
+        copied straight into its view of the θ arena (and a CPU .grad into the wire arena), so
+        the HBM never holds a second whole copy of the model."""
         if wire not in OUTER_WIRES:
             raise ValueError(f"wire {wire!r}: one of {OUTER_WIRES}")
         if exchange not in OUTER_EXCHANGES:
@@ -646,7 +649,7 @@ class DeviceOuterMirror:
         self.k = kernels or default_kernels()
         self.device = torch.device(device)
         for i, p in enumerate(self.params):
-            if p.device != self.device:
+            if p.device != self.device and not (keep_params and p.device.type == "cpu"):
                 raise ValueError(f"outer parameter {i} is on {p.device}, expected {self.device}")
             if p.dtype != torch.float32:
                 raise TypeError(f"outer parameter {i}: {p.dtype}, the outer step is fp32")
@@ -681,7 +684,18 @@ class DeviceOuterMirror:
         # the outer parameters share d_theta's version counter (OuterParameters made over its
         # views): θ's version is one integer; parameters kept in place keep their own counters
         self._shared_ver = fused and not keep_params
+        host_grads = None
+        if any(p.device != self.device for p in self.params):  # keep_params on CPU tensors
+            host_grads = [_GRAD.__get__(p) for p in self.params]
+            for p in self.params:
+                _GRAD.__set__(p, None)
         self._relay_theta()
+        if host_grads is not None:
+            with torch.no_grad():
+                for p, g, v in zip(self.params, host_grads, self._views["wire"]):
+                    if g is not None:
+                        v.copy_(g)
+                        _GRAD.__set__(p, v)
         if fused:
             self._install_outer_parameters(outer_model, keep_params)
         self._delta = None   # pending pseudo-gradient: (inner params, ptrs, versions, θ versions)

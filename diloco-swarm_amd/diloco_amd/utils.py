@@ -116,8 +116,9 @@ def outer_mirror(outer_model: nn.Module, device=None):
                 if device is None:
                     raise RuntimeError("the device outer model gets its device from the inner "
                                        "model's first compute_pseudo_gradient on the GPU")
+                # its CPU parameters go straight into the HBM arena, tensor by tensor
+                # (DeviceOuterMirror keep_params): no whole-model device copy first
                 dev = torch.device(device)
-                _move_params(outer_model, dev)
                 object.__setattr__(outer_model, _PENDING, False)
             cap = int(os.environ.get("DILOCO_OUTER_BUCKET_ELEMS", DEFAULT_BUCKET_CAP_ELEMS))
             m = DeviceOuterMirror(outer_model, dev, kernels=k, bucket_cap_elems=cap,
@@ -147,16 +148,6 @@ def outer_mirror(outer_model: nn.Module, device=None):
             m = HostOuterMirror(outer_model, torch.device(device), kernels=k, write_back=wb)
         object.__setattr__(outer_model, _ATTR, m)  # not a submodule / not in state_dict
     return m
-
-
-def _move_params(model: nn.Module, device: torch.device) -> None:
-    """Every parameter (and gradient) of `model` onto `device`, the Parameter objects kept
-    (an optimizer built on them stays valid)."""
-    with torch.no_grad():
-        for p in module_params(model):
-            p.data = p.data.to(device)
-            if p.grad is not None:
-                p.grad = p.grad.to(device)
 
 
 def _inner_device(inner_model: nn.Module) -> torch.device:

@@ -5,7 +5,7 @@ the inner one is still on the CPU (src/train.py:382; the inner model moves at :1
 get_outer_model(..., placement="device") on a CPU inner model must not place the outer model
 on torch.cuda.current_device() -- cuda:0 on every rank of a node -- but wait for the inner
 model's device, and TrainingComm(transport="device") defaults to cuda:local_rank. CPU-only:
-the GPU steps are faked at the seams (the mirror class, the parameter move); the real path
+the GPU steps are faked at the seams (the mirror class); the real path
 runs in tests/test_dropin_gpu.py (_outer_steps, placement="device")."""
 import os
 import tempfile
@@ -36,7 +36,7 @@ def test_device_outer_model_takes_the_inner_models_device(monkeypatch, current_d
     assert not utils.has_mirror(outer)
     assert all(p.device.type == "cpu" for p in outer.parameters())
     opt = get_optimizer(outer, _Cfg(type="SGD", lr=0.7, momentum=0.9, nesterov=True))
-    made, moved = {}, []
+    made = {}
 
     class RecordingMirror:  # stands in for DeviceOuterMirror: records where it was built
         def __init__(self, model, device, kernels=None, bucket_cap_elems=0, fused=False,
@@ -49,12 +49,13 @@ def test_device_outer_model_takes_the_inner_models_device(monkeypatch, current_d
 
     cuda3 = torch.device("cuda", 3)
     monkeypatch.setattr(utils, "DeviceOuterMirror", RecordingMirror)
-    monkeypatch.setattr(utils, "_move_params", lambda model, dev: moved.append(dev))
     # the inner model has moved to cuda:3 (src/train.py:163 with local_rank 3)
     monkeypatch.setattr(utils, "_inner_device", lambda model: cuda3)
     monkeypatch.setattr(utils, "device_path", lambda t: True)
     compute_pseudo_gradient(inner, outer)
-    assert made["device"] == cuda3 and moved == [cuda3]
+    assert made["device"] == cuda3
+    # no whole-model device copy first: the mirror gets the CPU parameters
+    assert all(p.device.type == "cpu" for p in made["params"])
     assert made["keep"]  # the optimizer's Parameter objects stay the outer model's
     assert all(a is b for a, b in zip(made["params"], opt.param_groups[0]["params"]))
     assert made["delta"] == 4
