@@ -626,14 +626,13 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
     spec = get_tree(tree)
     picks = _picks(tree == "t125", spec)
     init = spec.init_spec()
-    exp, own = {}, {}
+    exp = {}
     for t, lo, m in picks:  # the oracle on the sampled tensors: θ, buf and g per step
         b, sc = init[t]
         th = (F32(b) + synth.uniform(synth.OUTER_SEED, t, m, start=lo) * F32(sc)).astype(F32)
         buf = np.empty_like(th)
         for s in range(1, steps + 1):
             d = [oracle.delta(th, x) for x in _slice_inputs(t, lo, m, s, world, th)]
-            own[(t, s)] = d[rank].copy()
             if wire == "bf16":
                 acc = oracle.bf16_round(d[0])
                 for dr in d[1:]:
@@ -660,6 +659,12 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
     bad, lost = [], []
     digest = hashlib.sha256()
     for s in range(1, steps + 1):
+        # this rank's own delta as the pack must produce it, from the θ the device holds before
+        # the step (beyond two peers θ differs from the oracle's rank-order chain in the last
+        # bits -- gloo's sum order -- so the chain's delta is not the pack's bit pattern)
+        own = {t: oracle.delta(th0, _slice_inputs(t, lo, m, s, world, th0)[rank])
+               for t, lo, m in picks
+               for th0 in [list(outer.parameters())[t].detach().view(-1)[lo:lo + m].cpu().numpy()]}
         # θ on the device (the default placement's outer parameters are CPU tensors)
         th = [p.detach().view(-1).to("cuda:0") for p in outer.parameters()]
         inner_tree_device_verified(th, s, rank, [p.data.view(-1) for p in inner.parameters()])
@@ -671,7 +676,7 @@ def _full_size_dropin_two_peers(rank, world, steps=2, wire="f32", tree="t125",
         torch.cuda.synchronize()
         ops, ips = list(outer.parameters()), list(inner.parameters())
         for t, lo, m in picks:
-            nl = _lost_pack(snaps, t, own[(t, s)], wire == "bf16")
+            nl = _lost_pack(snaps, t, own[t], wire == "bf16")
             if nl:
                 lost.append((s, t, nl))
             want_th, want_buf, want_g = exp[(t, s)]
