@@ -165,36 +165,31 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 // DL_TUNE_AUTO selects: non-temporal loads with plain or non-temporal stores. `make TUNING=1`
 // (-DDL_TUNING) instantiates the whole matrix -- plain loads, write-through for every body --
 // for the measurement tools (tools/cold_sweep.py); dl_tree_tune rejects the rest otherwise.
-// Workgroup -> chunk. The dispatcher hands workgroup b to XCD b mod 8, so by default the
-// eight XCDs walk the range interleaved chunk by chunk. DL_XCD_CONTIG (A/B build,
-// tools/store_order_ab.py): with one workgroup per chunk, XCD x takes the x-th eighth of the
-// range instead, in order (n = 8q + r: XCDs below r take q + 1 chunks).
-// DL_XCD_BLOCK=B (A/B build): XCD x takes runs of B consecutive chunks -- its k-th
-// workgroup the chunk ((k / B) * 8 + x) * B + k % B -- over the whole super-blocks of 8B
-// chunks, the tail as by default (a bijection on [0, n)).
-__device__ __forceinline__ int32_t walk_index(int32_t b, int32_t n) {
-#ifdef DL_XCD_CONTIG
-  if (int32_t(gridDim.x) == n) {
-    const int32_t q = n >> 3, r = n & 7, x = b & 7, k = b >> 3;
+// Workgroup -> chunk. The dispatcher hands workgroup b to XCD (b + k) mod 8 (k fixed within a
+// dispatch: tools/fill_census.hip), so by default the eight XCDs walk the range interleaved
+// chunk by chunk. With one workgroup per chunk, xlog > 0 makes XCD x walk runs of B = 2^xlog
+// consecutive chunks -- its k-th workgroup takes chunk ((k >> xlog) * 8 + x) * B + (k & (B-1))
+// -- over the whole super-blocks of 8B chunks, the tail as by default; xlog = -1 gives XCD x
+// the x-th eighth of the range in order (n = 8q + r: XCDs below r take q + 1 chunks). Both
+// are bijections on [0, n). Measured on dl_delta_pack_sgd (tools/store_order_ab.py).
+__device__ __forceinline__ int32_t walk_index(int32_t b, int32_t n, int32_t xlog) {
+  if (xlog == 0 || int32_t(gridDim.x) != n) return b;
+  const int32_t x = b & 7, k = b >> 3;
+  if (xlog < 0) {
+    const int32_t q = n >> 3, r = n & 7;
     return x * q + (x < r ? x : r) + k;
   }
-#elif defined(DL_XCD_BLOCK)
-  constexpr int32_t B = DL_XCD_BLOCK;
-  const int32_t full = n / (8 * B) * (8 * B);
-  if (int32_t(gridDim.x) == n && b < full) {
-    const int32_t x = b & 7, k = b >> 3;
-    return ((k / B) * 8 + x) * B + k % B;
-  }
-#endif
-  return b;
+  const int32_t full = (n >> (xlog + 3)) << (xlog + 3);
+  if (b >= full) return b;
+  return (((k >> xlog) << 3) + x) * (1 << xlog) + (k & ((1 << xlog) - 1));
 }
 
 template <class Body, bool NTL, int NTS>
 __global__ void __launch_bounds__(kThreads)
     k_walk(const Chunk* __restrict__ chunks, int32_t c0, int32_t c1, void* const* __restrict__ caddr,
-           int32_t nchunk, Body body) {
+           int32_t nchunk, int32_t xlog, Body body) {
   for (int32_t i0 = int32_t(blockIdx.x); i0 < c1 - c0; i0 += int32_t(gridDim.x)) {
-    const int32_t c = c0 + walk_index(i0, c1 - c0);
+    const int32_t c = c0 + walk_index(i0, c1 - c0, xlog);
     const Chunk ck = chunks[c];
     body.template run<NTL, NTS>(ck, c, caddr, nchunk, int(threadIdx.x));
   }
@@ -215,7 +210,7 @@ __device__ __forceinline__ void sgd1(float g, float& buf, float& th, const SgdAr
 template <class Body, bool NTL, int NTS>
 hipError_t launch_walk(const Launch& L, const Body& body, int32_t grid) {
   hipLaunchKernelGGL((k_walk<Body, NTL, NTS>), dim3(grid), dim3(kThreads), 0, L.stream, L.chunks,
-                     L.c0, L.c1, L.caddr, L.nchunk, body);
+                     L.c0, L.c1, L.caddr, L.nchunk, L.xlog, body);
   return hipGetLastError();
 }
 

@@ -40,6 +40,10 @@ struct Launch {
   int32_t flags;  // DL_TUNE_*
   hipStream_t stream;
   bool pairs;  // two chunks per workgroup, loads of both before the stores (run_pairs)
+  // workgroup -> chunk mapping with one workgroup per chunk (walk_index, dl_device.h): XCD x
+  // walks runs of 2^xlog consecutive chunks (0: one chunk, the dispatcher's own interleave;
+  // -1: one contiguous eighth of the range per XCD)
+  int32_t xlog;
 };
 
 // peers of the direct exchange (dl_xgmi.hip): each rank's packed wire and θ, IPC-mapped

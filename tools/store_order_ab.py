@@ -9,14 +9,16 @@ into ONE process (ctypes, each its own copy of the library), and times the kerne
 variant on the same buffers, interleaved round by round, with HIP events on the stream the
 kernels are launched on:
 
-  base        the product build (SGD arithmetic, then wire, θ, momentum, inner; NT stores)
+  base        the product build (SGD arithmetic, then wire, θ, momentum, inner; NT stores;
+              from round 6, XCD runs of 16 chunks below 2^28 elements)
   plain       the product build with plain stores (dl_tree_tune(NT loads only))
   wire_first  the wire's rows stored right after the subtraction, before the SGD arithmetic
   rows        row by row across the four streams (wire, θ, momentum, inner per float4 row)
   reverse     inner, momentum, θ, then the wire
   wire_plain  the wire stored plainly, θ / momentum / inner non-temporally
   xcd_contig  XCD x walks the x-th eighth of the chunk range in order (not interleaved)
-  xcd_b<B>    XCD x walks runs of B consecutive chunks (B = 1 is the default interleave)
+  xcd_b<B>    XCD x walks runs of B consecutive chunks at every size (xcd_b1: the
+              dispatcher's interleave, the product's mapping up to round 5)
 
     python tools/store_order_ab.py --build                  # here (hipcc, no GPU)
     python tools/store_order_ab.py --tree t1.3b --rounds 6  # on the GPU box
@@ -39,10 +41,11 @@ FLAGS = ("--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fvisibility=hidden
 SRCS = ["dl_kernels.hip", "dl_q8.hip", "dl_xgmi.hip", "dl_comm.hip", "dl_abi.hip"]
 VARIANTS = {"base": [], "wire_first": ["-DDL_DPS_ORDER=1"], "rows": ["-DDL_DPS_ORDER=2"],
             "reverse": ["-DDL_DPS_ORDER=3"], "wire_plain": ["-DDL_DPS_WIRE_PLAIN"],
-            "xcd_contig": ["-DDL_XCD_CONTIG"], "xcd_b4": ["-DDL_XCD_BLOCK=4"],
-            "xcd_b8": ["-DDL_XCD_BLOCK=8"], "xcd_b16": ["-DDL_XCD_BLOCK=16"], "xcd_b32": ["-DDL_XCD_BLOCK=32"],
-            "xcd_b64": ["-DDL_XCD_BLOCK=64"], "xcd_b256": ["-DDL_XCD_BLOCK=256"],
-            "xcd_b2048": ["-DDL_XCD_BLOCK=2048"]}
+            "xcd_b1": ["-DDL_XCD_XLOG=0"], "xcd_contig": ["-DDL_XCD_XLOG=-1"],
+            "xcd_b4": ["-DDL_XCD_XLOG=2"], "xcd_b8": ["-DDL_XCD_XLOG=3"],
+            "xcd_b16": ["-DDL_XCD_XLOG=4"], "xcd_b32": ["-DDL_XCD_XLOG=5"],
+            "xcd_b64": ["-DDL_XCD_XLOG=6"], "xcd_b256": ["-DDL_XCD_XLOG=8"],
+            "xcd_b2048": ["-DDL_XCD_XLOG=11"]}
 DL_TUNE_NT_LOADS = 1
 
 
