@@ -738,8 +738,9 @@ def parity_sharded(dev, ws, rank, exchange="rccl"):
 
 
 def parity_dropin_exchanges(dev, ws, rank):
-    """The headline path's exchanges behind the reference's calls at N > 1: the fused device
-    outer model with exchange="sharded" (the default) and "a2a" against "replicated", tiny tree
+    """The exchanges behind the reference's calls at N > 1: the outer model get_outer_model
+    returns, with exchange="sharded" (opt-in here) and "a2a" against "replicated" (the
+    headline's, the default placement's default), tiny tree
     in 4 MiB buckets, 2 outer steps: θ, .grad, the momentum buffers (the sharded ones
     gathered on read) and the inner params normwise <= 1e-6 per tensor (bit-exact at n <= 2), every
     replica identical."""
