@@ -389,13 +389,6 @@ constexpr int32_t kAutoDeltaQ8 = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // cached, so they store non-temporally (dl_scatter and dl_unpack_avg also take two chunks per
 // workgroup there: 6 % faster flushed, profiles/r03_cold_sweep_flushed_t13b.json).
 constexpr int32_t kBigLaunchChunks = (1 << 28) / DL_CHUNK_ELEMS;
-// dl_delta_pack_sgd (the one-replica headline) below 2^28 elements under DL_TUNE_AUTO, one
-// workgroup per chunk: each XCD walks runs of 16 consecutive chunks instead of every eighth
-// chunk (walk_index). T125, interleaved A/B against the default on three boxes
-// (profiles/r06_store_order_ab_t125_{b,c,d}.json): runs of 16 +2.0 / +1.7 %, of 8 +1.4 %,
-// of 32 +2.4 / +0.4 / -0.1 %, of 64 -2.4 %, one contiguous eighth per XCD -5 %; over 2^28
-// elements (T1.3B) no mapping gains on every box, so those launches keep the interleave.
-constexpr int32_t kDeltaPackSgdXlog = 4;
 constexpr int32_t kAutoUnpackSgd = DL_TUNE_NT_LOADS | DL_TUNE_NT_STORES;
 // Kernels whose output no kernel re-reads next (dl_scatter: the inner params; dl_unpack_avg:
 // gradients; dl_unpack_sgd_q8: θ, momentum, inner) store non-temporally at every size. Round 2
@@ -433,6 +426,8 @@ int make_launch(dl_tree_t t, int32_t b, dl_stream_t s, dl::Launch* L, const char
 #ifdef DL_XCD_XLOG  // A/B builds (tools/store_order_ab.py): one mapping for every launch
   L->xlog = DL_XCD_XLOG;
 #else
+  // the dispatcher's interleave: runs of B chunks per XCD change the headline kernel's time by
+  // -3.4 ... +2.0 % depending on the box (profiles/r06_store_order_ab_*)
   L->xlog = 0;
 #endif
   if (t->flags == DL_TUNE_AUTO && big != Big::keep && L->c1 - L->c0 >= kBigLaunchChunks) {
@@ -543,10 +538,6 @@ DL_API int dl_delta_pack_sgd(dl_tree_t t, int32_t b, int32_t inner_slot, float* 
                              int32_t nesterov, int32_t first_step, dl_stream_t s) {
   dl::Launch L;
   DL_TRY(make_launch(t, b, s, &L, "dl_delta_pack_sgd", kAutoUnpackSgd));
-#ifndef DL_XCD_XLOG
-  if (t->flags == DL_TUNE_AUTO && L.grid == 0 && L.c1 - L.c0 < kBigLaunchChunks)
-    L.xlog = kDeltaPackSgdXlog;
-#endif
   DL_TRY(check_slot(t, inner_slot, "dl_delta_pack_sgd"));
   DL_TRY(check_packed(outer, "dl_delta_pack_sgd", "outer"));
   DL_TRY(check_packed(wire, "dl_delta_pack_sgd", "wire"));

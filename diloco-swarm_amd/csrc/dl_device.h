@@ -171,7 +171,8 @@ __device__ __forceinline__ T* slot_ptr(void* const* caddr, int nchunk, int slot,
 // consecutive chunks -- its k-th workgroup takes chunk ((k >> xlog) * 8 + x) * B + (k & (B-1))
 // -- over the whole super-blocks of 8B chunks, the tail as by default; xlog = -1 gives XCD x
 // the x-th eighth of the range in order (n = 8q + r: XCDs below r take q + 1 chunks). Both
-// are bijections on [0, n). Measured on dl_delta_pack_sgd (tools/store_order_ab.py).
+// are bijections on [0, n). The product launches with xlog = 0; the others are A/B builds
+// (tools/store_order_ab.py: no mapping gains on every box).
 __device__ __forceinline__ int32_t walk_index(int32_t b, int32_t n, int32_t xlog) {
   if (xlog == 0 || int32_t(gridDim.x) != n) return b;
   const int32_t x = b & 7, k = b >> 3;

@@ -407,39 +407,6 @@ def test_store_policies_are_bit_identical(kernel, misaligned):
     ref.close()
 
 
-@pytest.mark.parametrize("chunks", [1, 9, 127, 128, 129, 255, 256, 257, 1031, 2048])
-def test_delta_pack_sgd_xcd_runs_cover_every_chunk_once(chunks):
-    """Round 6: under DL_TUNE_AUTO dl_delta_pack_sgd below 2^28 elements maps workgroups to
-    chunks in runs of 16 per XCD (walk_index; whole super-blocks of 128 chunks, the tail
-    interleaved). Every chunk must be stepped exactly once -- a chunk stepped twice would
-    read θ' and come out wrong, one skipped would stay unchanged -- so the AUTO launch equals
-    the interleaved one (an explicit policy) bit for bit over two steps, for chunk counts on
-    both sides of the super-block boundaries and a ragged last chunk."""
-    sizes = [4096] * (chunks - 1) + [1000] if chunks > 1 else [333]
-    sizes = [sum(sizes[: len(sizes) // 2]), sum(sizes[len(sizes) // 2:])] if chunks > 8 else sizes
-    g0 = torch.Generator().manual_seed(41 + chunks)
-    host = [torch.randn(n, generator=g0) for n in sizes]
-    pa, pb = [h.to(DEV) for h in host], [h.to(DEV) for h in host]
-    ea = OuterSync(pa, world_size=1, fuse_single=True, keep_wire=True)  # AUTO: runs of 16
-    eb = OuterSync(pb, world_size=1, fuse_single=True, keep_wire=True)
-    eb.tree.tune(0, _lib.TUNE_NT_LOADS | _lib.TUNE_NT_STORES)  # same stores, interleaved
-    for _ in range(2):
-        noise = [torch.randn(n, generator=g0).to(DEV) * 1e-3 for n in sizes]
-        for p, q, z in zip(pa, pb, noise):
-            p.add_(z)
-            q.add_(z)
-        ea.step()
-        eb.step()
-        torch.cuda.synchronize()
-        assert torch.equal(ea.theta.view(torch.int32), eb.theta.view(torch.int32))
-        assert torch.equal(ea.mom.view(torch.int32), eb.mom.view(torch.int32))
-        assert torch.equal(ea.wire.view(torch.int32), eb.wire.view(torch.int32))
-        for p, q in zip(pa, pb):
-            assert torch.equal(p.view(torch.int32), q.view(torch.int32))
-    ea.close()
-    eb.close()
-
-
 def test_delta_pack_sgd_micro_matches_reference():
     """The one-pass step with the wire kept reproduces the reference's outer steps AND its
     outer.grad (the wire holds delta_s{s}_r0 after step s), micro tree, n = 1."""

@@ -17,6 +17,8 @@ kernels are launched on:
   reverse     inner, momentum, θ, then the wire
   wire_plain  the wire stored plainly, θ / momentum / inner non-temporally
   xcd_contig  XCD x walks the x-th eighth of the chunk range in order (not interleaved)
+  base_again  the product build once more, timed as a variant of its own: the spread between
+              two identical kernels is the A/B's noise floor
   xcd_b<B>    XCD x walks runs of B consecutive chunks at every size (xcd_b1: the
               dispatcher's interleave, the product's mapping up to round 5)
 
@@ -111,9 +113,10 @@ def main():
     ptrs = (ctypes.c_uint64 * len(inner))(*[x.data_ptr() for x in inner])
     for name in libs:
         assert libs[name].dl_tree_bind(trees[name], 0, ptrs, len(inner), s) == 0
-    runs = [(n, n, None) for n in VARIANTS] + [("plain", "base", DL_TUNE_NT_LOADS)]
+    runs = [(n, n, None) for n in VARIANTS] + [("plain", "base", DL_TUNE_NT_LOADS),
+                                                ("base_again", "base", None)]
     if a.only:
-        keep = set(a.only.split(",")) | {"base"}
+        keep = set(a.only.split(",")) | {"base", "base_again"}
         runs = [r for r in runs if r[0] in keep]
 
     def launch(lib, tree):
@@ -124,7 +127,10 @@ def main():
     res = {r[0]: [] for r in runs}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for rnd in range(a.rounds + 1):  # round 0: warm-up of every variant
-        for label, name, flags in runs:
+        # the order rotates every round: a variant's position in the round (the first one runs
+        # right after the previous round's synchronize) must not bias its time
+        k = rnd % len(runs)
+        for label, name, flags in runs[k:] + runs[:k]:
             lib, tree = libs[name], trees[name]
             lib.dl_tree_tune(tree, 0, -1 if flags is None else flags)
             launch(lib, tree)
