@@ -91,6 +91,8 @@ def collective_read(group, what: str) -> None:
     import os
     from datetime import timedelta
 
+    if not dist.is_initialized():  # no job, no rendezvous store (a group emulated in-process)
+        return
     if group is None:
         group = dist.group.WORLD
     n = dist.get_world_size(group)
@@ -689,6 +691,7 @@ class DeviceOuterMirror:
             host_grads = [_GRAD.__get__(p) for p in self.params]
             for p in self.params:
                 _GRAD.__set__(p, None)
+            self._relay("theta", "data", force=True)
         self._relay_theta()
         if host_grads is not None:
             with torch.no_grad():
@@ -778,17 +781,19 @@ class DeviceOuterMirror:
                 return False
         return True
 
-    def _relay(self, kind: str, what: str, zero_fill_missing: bool = True) -> bool:
+    def _relay(self, kind: str, what: str, zero_fill_missing: bool = True,
+               force: bool = False) -> bool:
         """Make every parameter's `what` ("data" or "grad") the view of arena `kind`; True if
-        any arena content was replaced."""
-        if self._in_place(kind, what):
+        any arena content was replaced. force: skip the address check (parameters on another
+        device: empty tensors' addresses can coincide across devices)."""
+        if not force and self._in_place(kind, what):
             return False
         views = self._views[kind]
         with torch.no_grad():
             for i, p in enumerate(self.params):
                 v = views[i]
                 cur = _DATA.__get__(p) if what == "data" else _GRAD.__get__(p)
-                if cur is not None and cur.data_ptr() == v.data_ptr():
+                if cur is not None and cur.data_ptr() == v.data_ptr() and cur.device == v.device:
                     continue
                 if cur is None:
                     if not zero_fill_missing:

@@ -112,6 +112,9 @@ def _run_case(case, rank, world, dev):
                                     nesterov=nesterov))
     comm = TrainingComm(World.from_default_group(1), (1, 1, 8), None)
     m = outer_mirror(outer, dev)  # the device outer model takes the inner model's device
+    if c["placement"] == "device":  # its parameters now live in the HBM arena
+        assert all(p.device == torch.device(dev) for p in outer.parameters()), (
+            case, [str(p.device) for p in outer.parameters()])
     tree = getattr(m, "dev", m).tree
     st = oracle.OuterState(c["theta0"], lr=c["lr"], momentum=momentum, nesterov=nesterov)
     exact = c["exchange"] in ("a2a", "int8")
