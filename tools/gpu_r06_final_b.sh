@@ -9,5 +9,5 @@ timeout -k 10 420 python bench.py --detail gpurun_out/final/bench_detail_n1.json
 cat gpurun_out/final/bench_n1.json
 bash tools/gpu_prof_headline.sh > gpurun_out/final/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/final/prof.log; exit 1; }
 tail -2 gpurun_out/final/prof.log
-TAG=r06 LIMIT=560 bash tools/gpu_rehearse_n8.sh > gpurun_out/final/n8.log 2>&1 || { echo "n8 rehearsal failed"; tail -30 gpurun_out/final/n8.log; exit 1; }
+TAG=r06 LIMIT=480 bash tools/gpu_rehearse_n8.sh > gpurun_out/final/n8.log 2>&1 || { echo "n8 rehearsal failed"; tail -30 gpurun_out/final/n8.log; exit 1; }
 head -c 600 gpurun_out/bench_n8_gloo_r06.json
