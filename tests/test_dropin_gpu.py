@@ -725,6 +725,13 @@ def _check_eight_peers(recs):
     """Config #4 / #5 with eight processes: every rank's checks clean, its own packed delta
     exact (a lost pack is a failure, not a retry), all replicas bit-identical."""
     info = [f"rank {r}: GPU state {str(rec.get('gpu', ''))}" for r, rec in enumerate(recs)]
+    path = os.environ.get("DILOCO_TEST_RECORD")  # the record scripts keep the GPU's state
+    if path:
+        import json
+
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", ""),
+                                "ranks": [str(rec.get("gpu", "")) for rec in recs]}) + "\n")
     for r, rec in enumerate(recs):
         assert rec["checked"] == 22
         assert int(rec["lost_pack"][0][0]) < 0, (r, rec["lost_pack"].tolist(), info)
